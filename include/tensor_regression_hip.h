@@ -1,0 +1,156 @@
+/*
+ * tensor_regression_hip.h — C ABI of the MI355X (gfx950) CP tensor-regression hot path.
+ *
+ * This is the drop-in boundary for the reference's forward/gradient loop
+ * (kimerein/tensor_regression).  The reference has no FFI layer of its own: its hot path
+ * is the pure-Python/torch sequence
+ *
+ *     lin_model / model  ->  loss_fn + lambda_L2 * L2_penalty  ->  loss.backward()
+ *                        ->  optimizer.step()  ->  loss_running.append(loss.item())
+ *
+ * in standard_tensor_regression.py:458-470 (CP_linear_regression.fit_Adam) and
+ * multinomial_tensor_regression.py:453-465 (CP_logistic_regression.fit_Adam).  Each entry
+ * point below replaces one contiguous piece of that sequence; the Python package
+ * `tensor_regression_amd` binds them with ctypes (INTEGRATION.md shows the binding).
+ *
+ * Conventions
+ *   - Every pointer argument is DEVICE memory on the plan's device unless stated otherwise;
+ *     the library never frees memory it did not allocate.
+ *   - fp32 everywhere (the reference's multinomial class is fp32-only,
+ *     multinomial_tensor_regression.py:255; the standard class defaults to fp32, :206).
+ *   - X is sample-major and C-contiguous: X[n, i_1, ..., i_K], i.e. an (N x P) row-major
+ *     matrix with P = prod(dims).
+ *   - Parameter arena: the Kruskal factor list `Bcp` packed back to back in the reference's
+ *     list order, each factor (I_f x R) row-major, followed by the scalar bias for the
+ *     linear model: [A_1 | A_2 | ... | A_F | (bias)].  tr_plan_factor_offset() gives the
+ *     offsets; tr_plan_num_params() the total.
+ *   - Gradient arena: same layout as the parameter arena plus ONE trailing slot holding the
+ *     data loss, i.e. tr_plan_num_grads() = tr_plan_num_params() + 1.  Data-term gradients
+ *     are already normalised by the GLOBAL sample count (linear) or class-weight total
+ *     (multinomial), so the element-wise sum of the arenas of disjoint sample shards is the
+ *     full-data gradient — one all-reduce(sum) per iteration is the only exchange.
+ *   - `stream` is a hipStream_t passed as void*; all calls are asynchronous on it.
+ *   - Return value: 0 on success, < 0 invalid argument (TR_E_*), > 0 a hipError_t.
+ *     tr_last_error() returns a thread-local message for the last failure.
+ *   - `stop_flag` (int32 device scalar, may be NULL): when non-zero every kernel of the
+ *     iteration returns immediately.  tr_adam_step sets it when the reference's plateau
+ *     test fires (standard_tensor_regression.py:467-470), which lets the host enqueue many
+ *     iterations without a per-iteration host synchronisation.
+ */
+#ifndef TENSOR_REGRESSION_HIP_H
+#define TENSOR_REGRESSION_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TR_ABI_VERSION 1
+
+#define TR_MODEL_LINEAR 0      /* CP_linear_regression: y_hat = <X, [[w; Phi]]> + bias, MSE */
+#define TR_MODEL_MULTINOMIAL 1 /* CP_logistic_regression: softmax(<X, [[w; Phi]]>), CE(weight) */
+
+#define TR_MAX_FACTORS 8
+
+#define TR_E_ARG (-1)      /* invalid argument (shape/size/pointer) */
+#define TR_E_UNSUPPORTED (-2)
+#define TR_E_NOMEM (-3)
+
+typedef struct tr_plan tr_plan;
+
+/* Library ABI version (TR_ABI_VERSION). */
+int tr_abi_version(void);
+
+/* Thread-local message describing the most recent failure ("" if none). */
+const char* tr_last_error(void);
+
+/*
+ * Create a plan for one model shape on `device` and allocate its workspace.
+ * Replaces the shape bookkeeping of CP_linear_regression.__init__
+ * (standard_tensor_regression.py:204-303) / CP_logistic_regression.__init__
+ * (multinomial_tensor_regression.py:212-286).
+ *   model          TR_MODEL_LINEAR or TR_MODEL_MULTINOMIAL
+ *   n_feature_modes K = X.ndim - 1 (1 .. TR_MAX_FACTORS-1)
+ *   feature_dims   host array of K dims (I_1 .. I_K)
+ *   n_classes      multinomial: C (the extra factor has C rows); linear: ignored (use 1)
+ *   rank           R (1 .. 64)
+ *   max_rows       largest sample count later passed to tr_loss_grad (sizes the workspace)
+ *   non_negative   host array, one flag per factor (K linear / K+1 multinomial): softplus
+ *                  is applied to flagged factors (non_neg_fn, standard…py:53-85)
+ *   softplus_beta / softplus_threshold   torch.nn.functional.softplus kwargs
+ */
+int tr_plan_create(tr_plan** out, int device, int model, int n_feature_modes,
+                   const int64_t* feature_dims, int n_classes, int rank, int64_t max_rows,
+                   const int32_t* non_negative, float softplus_beta, float softplus_threshold);
+
+int tr_plan_destroy(tr_plan* plan);
+
+int64_t tr_plan_num_params(const tr_plan* plan); /* factors (+ bias) */
+int64_t tr_plan_num_grads(const tr_plan* plan);  /* num_params + 1 (data-loss slot) */
+int64_t tr_plan_factor_offset(const tr_plan* plan, int factor);
+int64_t tr_plan_workspace_bytes(const tr_plan* plan);
+/* Human-readable description of the kernel strategy chosen for this plan (host string). */
+const char* tr_plan_describe(const tr_plan* plan);
+
+/*
+ * Forward model only (predict path).
+ * Replaces lin_model (standard…py:87-130) — out[n] = <X_n, B> + bias — and model
+ * (multinomial…py:148-187) — out[n, c] = softmax_c(<X_n, B_c>) — where
+ * B = cp_to_tensor((weights, non_neg_fn(Bcp))).
+ *   out: n_rows floats (linear) or n_rows x C floats row-major (multinomial).
+ */
+int tr_forward(tr_plan* plan, const float* X, int64_t n_rows, const float* params,
+               const float* weights, float* out, void* stream);
+
+/*
+ * Data-term loss and gradient of one sample shard (forward + loss + backward).
+ * Replaces the forward, loss_fn and loss.backward() of one fit_Adam iteration
+ * (standard…py:460-462; multinomial…py:455-457) — WITHOUT the L2 term, which
+ * tr_adam_step / tr_finalize_grad add once after the cross-shard sum.
+ *   target      linear: float y[n_rows]; multinomial: int64 labels[n_rows] in [0, C)
+ *   class_weight multinomial: float[C] CrossEntropyLoss weights; linear: NULL
+ *   norm        linear: global N (MSELoss mean); multinomial: global sum_n cw[y_n]
+ *   grad_out    tr_plan_num_grads() floats, overwritten: data gradient of every parameter
+ *               (+ bias) and the data loss in the last slot.
+ *   yhat_out    optional (may be NULL): linear model output per row (n_rows floats).
+ */
+int tr_loss_grad(tr_plan* plan, const float* X, int64_t n_rows, const void* target,
+                 const float* class_weight, double norm, const float* params,
+                 const float* weights, float* grad_out, float* yhat_out,
+                 const int32_t* stop_flag, void* stream);
+
+/*
+ * L2 term + total loss only (no parameter update) — the closure value/gradient that
+ * torch.optim.LBFGS needs in fit() (standard…py:368-373, multinomial…py:357-362).
+ *   grad_total_out  num_params floats: data gradient + lambda * d(sum_k ||A_k||_F)/dA
+ *   loss_out        1 float: data loss + lambda * sum_k ||A_k||_F (L2_penalty, standard…py:180-196)
+ */
+int tr_finalize_grad(tr_plan* plan, const float* params, const float* grad,
+                     float lambda_l2, float* grad_total_out, float* loss_out, void* stream);
+
+/*
+ * One torch.optim.Adam / AMSGrad step on the whole parameter arena, preceded by the L2
+ * term and followed by the reference's bookkeeping:
+ *   loss_hist[hist_base + iter] = data loss + lambda * L2_penalty   (loss_running.append)
+ *   if iter > patience and sum(|diff(loss_hist[iter - patience : hist_base + iter + 1])|) < tol:
+ *       *stop_flag = iter + 1                                      (standard…py:467-470)
+ * Adam math follows torch/optim/adam.py _single_tensor_adam (torch 2.10):
+ *   g += wd * p; m = lerp(m, g, 1 - b1); v = v * b2 + (1 - b2) g^2;
+ *   vmax = max(vmax, v) if amsgrad; denom = sqrt(v or vmax) / sqrt(1 - b2^t) + eps;
+ *   p -= lr / (1 - b1^t) * m / denom.
+ *   step        1-based Adam step t for this iteration
+ *   loss_hist   fp64 device array (the reference's loss_running as python floats)
+ *   max_exp_avg_sq  may be NULL when amsgrad == 0
+ */
+int tr_adam_step(tr_plan* plan, float* params, const float* grad, float* exp_avg,
+                 float* exp_avg_sq, float* max_exp_avg_sq, float lambda_l2, double lr,
+                 double beta1, double beta2, double eps, double weight_decay, int amsgrad,
+                 int64_t step, double* loss_hist, int64_t hist_base, int64_t iter,
+                 int64_t patience, double tol, int32_t* stop_flag, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TENSOR_REGRESSION_HIP_H */

@@ -1,0 +1,244 @@
+"""Host-side engine: one gfx950 plan per model shape, the packed parameter arena and the
+device-resident fit loop shared by CP_linear_regression and CP_logistic_regression.
+
+Everything on the hot path goes through the C ABI (include/tensor_regression_hip.h); torch is
+used only for device memory, the current HIP stream and torch.distributed.  The reference's
+per-iteration `loss.item()` host sync (standard_tensor_regression.py:464) is replaced by a
+device loss history plus a device stop flag (the plateau test of :467-470 runs on the GPU), so
+the host enqueues `sync_every` iterations between synchronisations.
+"""
+import ctypes
+import math
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check, ptr
+
+_DEFAULT_SOFTPLUS = {"beta": 50, "threshold": 1}
+# torch.optim.Adam defaults (torch/optim/adam.py)
+_ADAM_DEFAULTS = dict(lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0, amsgrad=False,
+                      foreach=None, maximize=False, capturable=False, differentiable=False,
+                      fused=None, decoupled_weight_decay=False)
+
+
+def softplus_params(softplus_kwargs):
+    kw = _DEFAULT_SOFTPLUS if softplus_kwargs is None else softplus_kwargs
+    # torch.nn.functional.softplus defaults when a key is absent
+    return float(kw.get("beta", 1.0)), float(kw.get("threshold", 20.0))
+
+
+def adam_hparams(Adam_kwargs):
+    """Resolve Adam kwargs exactly like torch.optim.Adam(params, **Adam_kwargs)."""
+    if Adam_kwargs is None:
+        # reference quirk (standard_tensor_regression.py:442-453): the default dict is never
+        # assigned, so torch.optim.Adam(..., **None) raises this TypeError
+        raise TypeError("torch.optim.adam.Adam() argument after ** must be a mapping, not NoneType")
+    hp = dict(_ADAM_DEFAULTS)
+    for k, v in Adam_kwargs.items():
+        if k not in hp:
+            raise TypeError(f"Adam.__init__() got an unexpected keyword argument '{k}'")
+        hp[k] = v
+    lr = float(hp["lr"])
+    b1, b2 = (float(b) for b in hp["betas"])
+    eps, wd = float(hp["eps"]), float(hp["weight_decay"])
+    if not 0.0 <= lr:
+        raise ValueError(f"Invalid learning rate: {lr}")
+    if not 0.0 <= eps:
+        raise ValueError(f"Invalid epsilon value: {eps}")
+    if not 0.0 <= b1 < 1.0:
+        raise ValueError(f"Invalid beta parameter at index 0: {b1}")
+    if not 0.0 <= b2 < 1.0:
+        raise ValueError(f"Invalid beta parameter at index 1: {b2}")
+    if not 0.0 <= wd:
+        raise ValueError(f"Invalid weight_decay value: {wd}")
+    if hp["maximize"] or hp["decoupled_weight_decay"] or hp["differentiable"]:
+        raise NotImplementedError("maximize / decoupled_weight_decay / differentiable Adam are not "
+                                  "implemented by the gfx950 fit loop")
+    return dict(lr=lr, beta1=b1, beta2=b2, eps=eps, weight_decay=wd, amsgrad=bool(hp["amsgrad"]))
+
+
+def device_index(device):
+    d = torch.device(device)
+    if d.type != "cuda":
+        raise ValueError(
+            f"tensor_regression_amd runs the hot path on the GPU (HIP); got device '{device}'. "
+            "Use device='cuda' / 'cuda:N'.")
+    return d.index if d.index is not None else torch.cuda.current_device()
+
+
+def compute_device(X, model_device):
+    """HIP device the hot path runs on: X's device if X is on the GPU, else the model's device
+    if that is a GPU, else the current GPU (parameters may stay on the host; they are packed
+    into the device arena per fit and written back in place)."""
+    if isinstance(X, torch.Tensor) and X.device.type == "cuda":
+        return X.device.index if X.device.index is not None else torch.cuda.current_device()
+    d = torch.device(model_device)
+    if d.type == "cuda":
+        return d.index if d.index is not None else torch.cuda.current_device()
+    if not torch.cuda.is_available():
+        raise _lib.HipLibraryError("no HIP device available: the gfx950 hot path has no CPU fallback")
+    return torch.cuda.current_device()
+
+
+def stream_handle(dev):
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+class Plan:
+    """Owns one `tr_plan` (workspace + kernel strategy) for a model shape."""
+
+    def __init__(self, model, feature_dims, n_classes, rank, max_rows, non_negative, softplus_kwargs,
+                 device):
+        self.lib = _lib.load()
+        self.dev = device_index(device)
+        self.device_str = f"cuda:{self.dev}"
+        self.model = model
+        self.feature_dims = [int(d) for d in feature_dims]
+        self.n_classes = int(n_classes)
+        self.rank = int(rank)
+        self.max_rows = int(max_rows)
+        nf = len(self.feature_dims) + (1 if model == _lib.TR_MODEL_MULTINOMIAL else 0)
+        self.n_factors = nf
+        nn = [1 if bool(non_negative[f]) else 0 for f in range(nf)]
+        beta, thr = softplus_params(softplus_kwargs)
+        dims = (ctypes.c_int64 * len(self.feature_dims))(*self.feature_dims)
+        nna = (ctypes.c_int32 * nf)(*nn)
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.dev):
+            rc = self.lib.tr_plan_create(ctypes.byref(h), self.dev, model, len(self.feature_dims), dims,
+                                         self.n_classes, self.rank, max(1, self.max_rows), nna, beta, thr)
+        check(rc, "tr_plan_create")
+        self.h = h
+        self.num_params = int(self.lib.tr_plan_num_params(h))
+        self.num_grads = int(self.lib.tr_plan_num_grads(h))
+        self.offsets = [int(self.lib.tr_plan_factor_offset(h, f)) for f in range(nf + 1)]
+        self.describe = self.lib.tr_plan_describe(h).decode()
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h is not None and h.value:
+            try:
+                self.lib.tr_plan_destroy(h)
+            except Exception:
+                pass
+            self.h = None
+
+    # ---- parameter arena -------------------------------------------------------------------
+    def factor_shapes(self):
+        dims = self.feature_dims + ([self.n_classes] if self.model == _lib.TR_MODEL_MULTINOMIAL else [])
+        return [(d, self.rank) for d in dims]
+
+    def pack(self, Bcp, bias=None):
+        arena = torch.empty(self.num_params, dtype=torch.float32, device=f"cuda:{self.dev}")
+        shapes = self.factor_shapes()
+        if len(Bcp) != len(shapes):
+            raise ValueError(f"expected {len(shapes)} Kruskal factors, got {len(Bcp)}")
+        with torch.no_grad():
+            for f, (A, shp) in enumerate(zip(Bcp, shapes)):
+                A = torch.as_tensor(A)
+                if tuple(A.shape) != shp:
+                    raise ValueError(f"factor {f} has shape {tuple(A.shape)}, expected {shp}")
+                arena[self.offsets[f]:self.offsets[f + 1]].copy_(A.detach().reshape(-1))
+            if self.model == _lib.TR_MODEL_LINEAR:
+                arena[self.offsets[-1]:].copy_(torch.as_tensor(bias).detach().reshape(-1)[:1])
+        return arena
+
+    def unpack_into(self, arena, Bcp, bias=None):
+        """Write the arena back into the caller's tensors in place (like an optimizer step)."""
+        with torch.no_grad():
+            for f, A in enumerate(Bcp):
+                src = arena[self.offsets[f]:self.offsets[f + 1]].view(A.shape)
+                A.copy_(src.to(device=A.device, dtype=A.dtype))
+            if bias is not None and self.model == _lib.TR_MODEL_LINEAR:
+                bias.copy_(arena[self.offsets[-1]:].to(device=bias.device, dtype=bias.dtype).view(bias.shape))
+
+    def factor_views(self, arena):
+        return [arena[self.offsets[f]:self.offsets[f + 1]].view(shp)
+                for f, shp in enumerate(self.factor_shapes())]
+
+    # ---- entry points ------------------------------------------------------------------------
+    def forward(self, X, arena, weights, out=None):
+        N = X.shape[0]
+        C = self.n_classes if self.model == _lib.TR_MODEL_MULTINOMIAL else 1
+        if out is None:
+            shape = (N, C) if self.model == _lib.TR_MODEL_MULTINOMIAL else (N,)
+            out = torch.empty(shape, dtype=torch.float32, device=X.device)
+        rc = self.lib.tr_forward(self.h, ptr(X), N, ptr(arena), ptr(weights), ptr(out), stream_handle(self.dev))
+        check(rc, "tr_forward")
+        return out
+
+    def loss_grad(self, X, target, class_weight, norm, arena, weights, grad, yhat=None, stop=None):
+        rc = self.lib.tr_loss_grad(self.h, ptr(X), X.shape[0], ptr(target), ptr(class_weight), float(norm),
+                                   ptr(arena), ptr(weights), ptr(grad), ptr(yhat), ptr(stop),
+                                   stream_handle(self.dev))
+        check(rc, "tr_loss_grad")
+
+    def finalize_grad(self, arena, grad, lambda_l2, grad_total, loss_out):
+        rc = self.lib.tr_finalize_grad(self.h, ptr(arena), ptr(grad), float(lambda_l2), ptr(grad_total),
+                                       ptr(loss_out), stream_handle(self.dev))
+        check(rc, "tr_finalize_grad")
+
+    def adam_step(self, arena, grad, m, v, vmax, lambda_l2, hp, step, hist, hist_base, it, patience, tol,
+                  stop):
+        rc = self.lib.tr_adam_step(self.h, ptr(arena), ptr(grad), ptr(m), ptr(v), ptr(vmax), float(lambda_l2),
+                                   hp["lr"], hp["beta1"], hp["beta2"], hp["eps"], hp["weight_decay"],
+                                   1 if hp["amsgrad"] else 0, int(step), ptr(hist), int(hist_base), int(it),
+                                   int(patience), float(tol), ptr(stop), stream_handle(self.dev))
+        check(rc, "tr_adam_step")
+
+
+def as_device_f32(X, dev):
+    """X as a contiguous fp32 tensor on cuda:dev (copies only when needed)."""
+    if not isinstance(X, torch.Tensor):
+        X = torch.as_tensor(np.asarray(X), dtype=torch.float32)
+    if X.dtype != torch.float32:
+        raise TypeError(f"the gfx950 path computes in fp32; got X of dtype {X.dtype}")
+    if X.device.type != "cuda" or X.device.index != dev:
+        X = X.to(f"cuda:{dev}")
+    return X.contiguous()
+
+
+def run_adam_fit(plan, X, target, class_weight, norm, arena, weights, lambda_L2, max_iter, tol, patience,
+                 hp, loss_running, verbose_cb=None, allreduce=None, sync_every=64):
+    """The fit_Adam loop (standard…py:453-470 / multinomial…py:447-465), device resident.
+
+    Returns (convergence_reached, number_of_iterations_run).  `loss_running` is extended in place
+    with the reference's per-iteration losses.  `allreduce(grad)` (optional) sums the gradient
+    arena over sample shards between the local gradient and the Adam step.
+    """
+    dev = plan.device_str
+    opts = dict(dtype=torch.float32, device=dev)
+    grad = torch.zeros(plan.num_grads, **opts)
+    m = torch.zeros(plan.num_params, **opts)
+    v = torch.zeros(plan.num_params, **opts)
+    vmax = torch.zeros(plan.num_params, **opts) if hp["amsgrad"] else None
+    base = len(loss_running)
+    hist = torch.zeros(base + max(int(max_iter), 0) + 1, dtype=torch.float64, device=dev)
+    if base:
+        hist[:base] = torch.tensor(loss_running, dtype=torch.float64)
+    stop = torch.zeros(1, dtype=torch.int32, device=dev)
+    ii = 0
+    stopped_at = 0
+    if verbose_cb is not None:
+        sync_every = 1
+    while ii < max_iter:
+        n = min(sync_every, max_iter - ii)
+        for k in range(n):
+            it = ii + k
+            if verbose_cb is not None:
+                verbose_cb.before_step(arena)
+            plan.loss_grad(X, target, class_weight, norm, arena, weights, grad, stop=stop)
+            if allreduce is not None:
+                allreduce(grad)
+            plan.adam_step(arena, grad, m, v, vmax, lambda_L2, hp, it + 1, hist, base, it, patience, tol, stop)
+        ii += n
+        stopped_at = int(stop.item())  # one host sync per chunk
+        if verbose_cb is not None:
+            verbose_cb.after_step(ii - 1, float(hist[base + ii - 1].item()))
+        if stopped_at:
+            break
+    n_run = stopped_at if stopped_at else ii
+    loss_running.extend(hist[base:base + n_run].tolist())
+    return bool(stopped_at), n_run

@@ -1,0 +1,392 @@
+// tr_api.hip — the C ABI (include/tensor_regression_hip.h): plans, workspace, kernel strategy.
+//
+// A plan is the MI355X-side image of one CP_linear_regression / CP_logistic_regression shape
+// (standard_tensor_regression.py:204-303, multinomial_tensor_regression.py:212-286): the
+// Kruskal factor layout, the dense-coefficient workspace and the per-iteration scratch.
+// All device buffers the caller passes in are borrowed; the plan owns only its workspace.
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+#include "../../include/tensor_regression_hip.h"
+#include "tr_kernels.h"
+
+using namespace tr;
+
+struct tr_plan {
+  int device = 0;
+  int model = TR_MODEL_LINEAR;
+  int K = 0;  // feature modes
+  int C = 1;  // classes (1 for linear)
+  int R = 0;
+  int has_bias = 1;
+  float sp_beta = 50.f, sp_thr = 1.f;
+  int64_t P = 0, ncols = 0, nparams = 0, ngrads = 0, max_rows = 0;
+  FactorSet fs{};
+  int ncu = 256;
+  int W = 4;
+  // single-pass linear strategy
+  int fused = 0, fT = 0, fCH = 0, fgrid = 0;
+  // two-pass strategy
+  int64_t max_slabs = 0;
+  // workspace
+  void* ws = nullptr;
+  size_t ws_bytes = 0;
+  float *phi = nullptr, *dphi = nullptr, *dense = nullptr, *G = nullptr, *gpart = nullptr, *rowbuf = nullptr;
+  double* dpart = nullptr;
+  int64_t gpart_slabs = 0, dpart_n = 0;
+  unsigned parity = 0;
+  std::string desc;
+};
+
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+static int hip_fail(hipError_t e, const char* where) {
+  g_err = std::string(where) + ": " + hipGetErrorString(e);
+  return (int)e;
+}
+#define TR_HIP(expr)                                   \
+  do {                                                 \
+    hipError_t _e = (expr);                            \
+    if (_e != hipSuccess) return hip_fail(_e, #expr);  \
+  } while (0)
+
+static bool env_flag(const char* name) {
+  const char* v = std::getenv(name);
+  return v != nullptr && v[0] != '\0' && v[0] != '0';
+}
+
+extern "C" int tr_abi_version(void) { return TR_ABI_VERSION; }
+extern "C" const char* tr_last_error(void) { return g_err.c_str(); }
+
+// Single-pass strategy for the linear model: among the (T, CH) with P == 4*T*CH, keep the
+// spill-free instantiations and pick the one with the most X bytes in flight per CU (one
+// prefetched row per resident workgroup), ties to the smaller workgroup.
+static void choose_fused(tr_plan* p) {
+  p->fused = 0;
+  if (p->model != TR_MODEL_LINEAR || p->P % 4 != 0 || env_flag("TR_FORCE_TWOPASS")) return;
+  const int64_t P4 = p->P / 4;
+  const size_t lds_max = 160 * 1024;
+  const int Ts[5] = {64, 128, 256, 512, 1024};
+  int64_t best_bytes = 0;
+  for (int k = 0; k < 5; ++k) {
+    const int T = Ts[k];
+    if (P4 % T != 0) continue;
+    const int64_t CH = P4 / T;
+    if (!linear_fused_supported(T, (int)CH)) continue;
+    const size_t lds = (size_t)p->P * 4 + 2 * (T / 64) * 4;
+    if (lds > lds_max) continue;
+    int per_cu = 0;
+    if (prepare_linear_fused(T, (int)CH, lds, &per_cu) != hipSuccess || per_cu < 1) continue;
+    const int64_t bytes = (int64_t)per_cu * p->P * 4;
+    if (bytes > best_bytes) {
+      best_bytes = bytes;
+      p->fused = 1;
+      p->fT = T;
+      p->fCH = (int)CH;
+      p->fgrid = p->ncu * per_cu;
+    }
+  }
+}
+
+extern "C" int tr_plan_create(tr_plan** out, int device, int model, int n_feature_modes,
+                              const int64_t* feature_dims, int n_classes, int rank, int64_t max_rows,
+                              const int32_t* non_negative, float softplus_beta,
+                              float softplus_threshold) {
+  if (out == nullptr) return fail(TR_E_ARG, "out is NULL");
+  *out = nullptr;
+  if (model != TR_MODEL_LINEAR && model != TR_MODEL_MULTINOMIAL) return fail(TR_E_ARG, "unknown model");
+  const int nf = n_feature_modes + (model == TR_MODEL_MULTINOMIAL ? 1 : 0);
+  if (n_feature_modes < 1 || nf > TR_MAXF) return fail(TR_E_ARG, "number of factors out of range [1, 8]");
+  if (rank < 1 || rank > TR_MAXR) return fail(TR_E_ARG, "rank out of range [1, 64]");
+  if (feature_dims == nullptr) return fail(TR_E_ARG, "feature_dims is NULL");
+  if (max_rows < 1) return fail(TR_E_ARG, "max_rows must be >= 1");
+  const int C = model == TR_MODEL_MULTINOMIAL ? n_classes : 1;
+  if (C < 1) return fail(TR_E_ARG, "n_classes must be >= 1");
+  if (!rows_supported(C)) return fail(TR_E_UNSUPPORTED, "n_classes > 16 not supported by the gfx950 kernels yet");
+
+  tr_plan* p = new tr_plan();
+  p->device = device;
+  p->model = model;
+  p->K = n_feature_modes;
+  p->C = C;
+  p->R = rank;
+  p->has_bias = model == TR_MODEL_LINEAR;
+  p->sp_beta = softplus_beta;
+  p->sp_thr = softplus_threshold;
+  p->max_rows = max_rows;
+
+  int64_t P = 1;
+  for (int k = 0; k < n_feature_modes; ++k) {
+    if (feature_dims[k] < 1) {
+      delete p;
+      return fail(TR_E_ARG, "feature dims must be >= 1");
+    }
+    P *= feature_dims[k];
+  }
+  p->P = P;
+  p->ncols = P * C;
+  if (p->ncols >= ((int64_t)1 << 31)) {
+    delete p;
+    return fail(TR_E_UNSUPPORTED, "prod(dims) * n_classes must be < 2^31");
+  }
+  FactorSet& fs = p->fs;
+  std::memset(&fs, 0, sizeof(fs));
+  fs.nf = nf;
+  fs.rank = rank;
+  for (int f = 0; f < nf; ++f) {
+    fs.dim[f] = f < n_feature_modes ? feature_dims[f] : C;
+    fs.nonneg[f] = non_negative ? (non_negative[f] != 0) : 0;
+  }
+  int64_t off = 0, rs = 1;
+  for (int f = 0; f < nf; ++f) {
+    fs.off[f] = off;
+    off += fs.dim[f] * rank;
+  }
+  for (int f = nf - 1; f >= 0; --f) {
+    fs.rstride[f] = rs;
+    rs *= fs.dim[f];
+  }
+  fs.total = rs;
+  fs.nfelem = off;
+  // dense layout: row-major over feature modes; class factor (multinomial) slowest
+  int64_t ds = 1;
+  for (int f = n_feature_modes - 1; f >= 0; --f) {
+    fs.stride[f] = ds;
+    ds *= fs.dim[f];
+  }
+  if (model == TR_MODEL_MULTINOMIAL) fs.stride[n_feature_modes] = P;
+  p->nparams = fs.nfelem + (p->has_bias ? 1 : 0);
+  p->ngrads = p->nparams + 1;
+  p->W = (P % 4 == 0) ? 4 : 1;
+
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) {
+    delete p;
+    return hip_fail(e, "hipSetDevice");
+  }
+  int ncu = 0;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
+    p->ncu = ncu;
+
+  choose_fused(p);
+
+  // two-pass slab budget: max(16 MiB, 2 % of X bytes)
+  {
+    const double xbytes = (double)max_rows * (double)P * 4.0;
+    double budget = xbytes * 0.02;
+    if (budget < 16.0 * 1024 * 1024) budget = 16.0 * 1024 * 1024;
+    int64_t ms = (int64_t)(budget / ((double)p->ncols * 4.0));
+    if (ms < 1) ms = 1;
+    if (ms > 1024) ms = 1024;
+    p->max_slabs = ms;
+  }
+  p->gpart_slabs = p->max_slabs;
+  if (p->fused && p->fgrid > p->gpart_slabs) p->gpart_slabs = p->fgrid;
+  p->dpart_n = rows_num_waves(C, max_rows) + 64;
+  if (p->fused && p->fgrid > p->dpart_n) p->dpart_n = p->fgrid;
+
+  // workspace carve (256-B aligned pieces)
+  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  const size_t b_phi = al(fs.nfelem * 4), b_dense = al(p->ncols * 4), b_gpart = al((size_t)p->gpart_slabs * p->ncols * 4),
+               b_row = al((size_t)max_rows * C * 4), b_dpart = al((size_t)p->dpart_n * 2 * 8);
+  p->ws_bytes = 2 * b_phi + 2 * b_dense + b_gpart + b_row + b_dpart;
+  e = hipMalloc(&p->ws, p->ws_bytes);
+  if (e != hipSuccess) {
+    delete p;
+    return hip_fail(e, "hipMalloc(workspace)");
+  }
+  char* c = (char*)p->ws;
+  p->phi = (float*)c;
+  c += b_phi;
+  p->dphi = (float*)c;
+  c += b_phi;
+  p->dense = (float*)c;
+  c += b_dense;
+  p->G = (float*)c;
+  c += b_dense;
+  p->gpart = (float*)c;
+  c += b_gpart;
+  p->rowbuf = (float*)c;
+  c += b_row;
+  p->dpart = (double*)c;
+  TR_HIP(hipMemset(p->ws, 0, p->ws_bytes));
+
+  char buf[512];
+  std::snprintf(buf, sizeof(buf),
+                "model=%s K=%d C=%d R=%d P=%lld nparams=%lld ncu=%d path=%s T=%d CH=%d grid=%d W=%d "
+                "max_slabs=%lld workspace=%.1fMiB",
+                model == TR_MODEL_LINEAR ? "linear" : "multinomial", p->K, C, rank, (long long)P,
+                (long long)p->nparams, p->ncu, p->fused ? "fused-1pass" : "2pass", p->fT, p->fCH, p->fgrid,
+                p->W, (long long)p->max_slabs, p->ws_bytes / 1048576.0);
+  p->desc = buf;
+  *out = p;
+  return 0;
+}
+
+extern "C" int tr_plan_destroy(tr_plan* p) {
+  if (p == nullptr) return 0;
+  if (p->ws) {
+    (void)hipSetDevice(p->device);
+    (void)hipFree(p->ws);
+  }
+  delete p;
+  return 0;
+}
+
+extern "C" int64_t tr_plan_num_params(const tr_plan* p) { return p ? p->nparams : -1; }
+extern "C" int64_t tr_plan_num_grads(const tr_plan* p) { return p ? p->ngrads : -1; }
+extern "C" int64_t tr_plan_factor_offset(const tr_plan* p, int f) {
+  if (p == nullptr || f < 0 || f > p->fs.nf) return -1;
+  return f == p->fs.nf ? p->fs.nfelem : p->fs.off[f];
+}
+extern "C" int64_t tr_plan_workspace_bytes(const tr_plan* p) { return p ? (int64_t)p->ws_bytes : -1; }
+extern "C" const char* tr_plan_describe(const tr_plan* p) { return p ? p->desc.c_str() : ""; }
+
+static int factor_prep(tr_plan* p, const float* params, const float* w, const int32_t* stop, hipStream_t st) {
+  TR_HIP(launch_prep_factors(p->fs, params, p->sp_beta, p->sp_thr, p->phi, p->dphi, stop, st));
+  TR_HIP(launch_build_dense(p->fs, p->phi, w, p->dense, stop, st));
+  return 0;
+}
+
+extern "C" int tr_forward(tr_plan* p, const float* X, int64_t n_rows, const float* params, const float* weights,
+                          float* out, void* stream) {
+  if (p == nullptr) return fail(TR_E_ARG, "plan is NULL");
+  if (X == nullptr || params == nullptr || weights == nullptr || out == nullptr)
+    return fail(TR_E_ARG, "NULL buffer");
+  if (n_rows < 1) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  TR_HIP(hipSetDevice(p->device));
+  int rc = factor_prep(p, params, weights, nullptr, st);
+  if (rc) return rc;
+  const int mode = p->model == TR_MODEL_LINEAR ? MODE_LIN_PRED : MODE_MNL_PRED;
+  TR_HIP(launch_rows(p->C, mode, p->W, X, n_rows, p->P, p->dense, params + p->fs.nfelem, nullptr, nullptr, 0.f,
+                     out, nullptr, nullptr, nullptr, st));
+  return 0;
+}
+
+extern "C" int tr_loss_grad(tr_plan* p, const float* X, int64_t n_rows, const void* target,
+                            const float* class_weight, double norm, const float* params, const float* weights,
+                            float* grad_out, float* yhat_out, const int32_t* stop_flag, void* stream) {
+  if (p == nullptr) return fail(TR_E_ARG, "plan is NULL");
+  if (X == nullptr || target == nullptr || params == nullptr || weights == nullptr || grad_out == nullptr)
+    return fail(TR_E_ARG, "NULL buffer");
+  if (p->model == TR_MODEL_MULTINOMIAL && class_weight == nullptr)
+    return fail(TR_E_ARG, "multinomial model needs class_weight");
+  if (n_rows < 0 || n_rows > p->max_rows) return fail(TR_E_ARG, "n_rows exceeds the plan's max_rows");
+  if (!(norm > 0.0)) return fail(TR_E_ARG, "norm must be > 0");
+  hipStream_t st = (hipStream_t)stream;
+  TR_HIP(hipSetDevice(p->device));
+  if (n_rows == 0) {
+    // an empty shard contributes nothing to the all-reduced sum
+    TR_HIP(hipMemsetAsync(grad_out, 0, (size_t)p->ngrads * 4, st));
+    return 0;
+  }
+  int rc = factor_prep(p, params, weights, stop_flag, st);
+  if (rc) return rc;
+  const int64_t N = n_rows;
+  float* loss_slot = grad_out + p->nparams;
+  float* bias_slot = p->has_bias ? grad_out + p->fs.nfelem : nullptr;
+  const float* bias = p->has_bias ? params + p->fs.nfelem : nullptr;
+  const int reverse = (int)(p->parity & 1u);
+  p->parity++;
+
+  if (p->fused) {
+    if (yhat_out != nullptr)  // the single-pass kernel does not emit y_hat; one extra forward pass
+      TR_HIP(launch_rows(1, MODE_LIN_PRED, p->W, X, N, p->P, p->dense, bias, nullptr, nullptr, 0.f, yhat_out,
+                         nullptr, nullptr, stop_flag, st));
+    const int64_t rpw = (N + p->fgrid - 1) / p->fgrid;
+    TR_HIP(launch_linear_fused(p->fT, p->fCH, p->fgrid, X, N, p->P, p->dense, bias, (const float*)target,
+                               (float)(2.0 / norm), p->gpart, p->dpart, yhat_out, rpw, reverse, stop_flag, st));
+    TR_HIP(launch_reduce_slabs(4, p->gpart, p->fgrid, p->P, p->G, p->dpart, p->fgrid, 1.0 / norm, loss_slot,
+                               bias_slot, stop_flag, st));
+  } else {
+    const int C = p->C;
+    if (p->model == TR_MODEL_LINEAR) {
+      TR_HIP(launch_rows(1, MODE_LIN_TRAIN, p->W, X, N, p->P, p->dense, bias, target, nullptr,
+                         (float)(2.0 / norm), p->rowbuf, p->dpart, yhat_out, stop_flag, st));
+    } else {
+      TR_HIP(launch_rows(C, MODE_MNL_TRAIN, p->W, X, N, p->P, p->dense, nullptr, target, class_weight,
+                         (float)(1.0 / norm), p->rowbuf, p->dpart, nullptr, stop_flag, st));
+    }
+    const int64_t nd = rows_num_waves(C, N);
+    const int cw = cols_cw(C);
+    const int64_t PW = p->P / p->W;
+    const int64_t nstripes = (PW + 256 * cw - 1) / (256 * cw);
+    int64_t nchunks = (2048 + nstripes - 1) / nstripes;
+    if (nchunks > p->max_slabs) nchunks = p->max_slabs;
+    const int64_t by_rows = (N + 15) / 16;
+    if (nchunks > by_rows) nchunks = by_rows;
+    if (nchunks < 1) nchunks = 1;
+    const int64_t rpc = (N + nchunks - 1) / nchunks;
+    nchunks = (N + rpc - 1) / rpc;
+    TR_HIP(launch_cols(C, p->W, nstripes, nchunks, X, N, p->P, p->rowbuf, rpc, p->gpart, 1, stop_flag, st));
+    TR_HIP(launch_reduce_slabs(p->W, p->gpart, nchunks, p->ncols, p->G, p->dpart, nd, 1.0 / norm, loss_slot,
+                               bias_slot, stop_flag, st));
+  }
+  TR_HIP(launch_mttkrp(p->fs, p->phi, p->dphi, weights, p->G, grad_out, stop_flag, st));
+  return 0;
+}
+
+static UpdateArgs make_args(float lambda_l2) {
+  UpdateArgs ua;
+  std::memset(&ua, 0, sizeof(ua));
+  ua.lambda_l2 = lambda_l2;
+  ua.bc2_sqrt = 1.f;
+  return ua;
+}
+
+extern "C" int tr_finalize_grad(tr_plan* p, const float* params, const float* grad, float lambda_l2,
+                                float* grad_total_out, float* loss_out, void* stream) {
+  if (p == nullptr) return fail(TR_E_ARG, "plan is NULL");
+  if (params == nullptr || grad == nullptr || grad_total_out == nullptr) return fail(TR_E_ARG, "NULL buffer");
+  TR_HIP(hipSetDevice(p->device));
+  UpdateArgs ua = make_args(lambda_l2);
+  ua.mode = 1;
+  TR_HIP(launch_update(p->fs, p->has_bias, const_cast<float*>(params), grad, ua, nullptr, nullptr, nullptr,
+                       grad_total_out, loss_out, nullptr, nullptr, (hipStream_t)stream));
+  return 0;
+}
+
+extern "C" int tr_adam_step(tr_plan* p, float* params, const float* grad, float* exp_avg, float* exp_avg_sq,
+                            float* max_exp_avg_sq, float lambda_l2, double lr, double beta1, double beta2,
+                            double eps, double weight_decay, int amsgrad, int64_t step, double* loss_hist,
+                            int64_t hist_base, int64_t iter, int64_t patience, double tol, int32_t* stop_flag,
+                            void* stream) {
+  if (p == nullptr) return fail(TR_E_ARG, "plan is NULL");
+  if (params == nullptr || grad == nullptr || exp_avg == nullptr || exp_avg_sq == nullptr)
+    return fail(TR_E_ARG, "NULL buffer");
+  if (amsgrad && max_exp_avg_sq == nullptr) return fail(TR_E_ARG, "amsgrad needs max_exp_avg_sq");
+  if (step < 1) return fail(TR_E_ARG, "step must be >= 1");
+  TR_HIP(hipSetDevice(p->device));
+  UpdateArgs ua = make_args(lambda_l2);
+  ua.mode = 0;
+  ua.amsgrad = amsgrad ? 1 : 0;
+  // torch/optim/adam.py (non-capturable): python-float arithmetic, then fp32 scalars
+  const double st = (double)step;
+  const double bc1 = 1.0 - std::pow(beta1, st);
+  const double bc2 = 1.0 - std::pow(beta2, st);
+  ua.step_size = (float)(lr / bc1);
+  ua.bc2_sqrt = (float)std::pow(bc2, 0.5);
+  ua.one_minus_b1 = (float)(1.0 - beta1);
+  ua.beta2 = (float)beta2;
+  ua.one_minus_b2 = (float)(1.0 - beta2);
+  ua.eps = (float)eps;
+  ua.weight_decay = (float)weight_decay;
+  ua.hist_base = hist_base;
+  ua.iter = iter;
+  ua.patience = patience;
+  ua.tol = tol;
+  TR_HIP(launch_update(p->fs, p->has_bias, params, grad, ua, exp_avg, exp_avg_sq, max_exp_avg_sq, nullptr, nullptr,
+                       loss_hist, stop_flag, (hipStream_t)stream));
+  return 0;
+}

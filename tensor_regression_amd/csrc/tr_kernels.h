@@ -1,0 +1,64 @@
+// tr_kernels.h — host-side launch interface of the gfx950 kernels (internal, not the C ABI).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "tr_common.h"
+
+namespace tr {
+
+enum { MODE_LIN_TRAIN = 0, MODE_LIN_PRED = 1, MODE_MNL_TRAIN = 2, MODE_MNL_PRED = 3 };
+
+// Scalars of one k_update launch (Adam constants precomputed on the host in fp64 exactly
+// as torch/optim/adam.py does with python floats, then rounded to fp32 like torch's scalar
+// arguments).
+struct UpdateArgs {
+  int mode;            // 0 = Adam step, 1 = finalize only (LBFGS closure)
+  int amsgrad;
+  float lambda_l2;
+  float one_minus_b1;  // lerp weight
+  float beta2;
+  float one_minus_b2;
+  float eps;
+  float weight_decay;
+  float step_size;     // lr / (1 - b1^t)
+  float bc2_sqrt;      // sqrt(1 - b2^t)
+  int64_t hist_base;
+  int64_t iter;
+  int64_t patience;
+  double tol;
+};
+
+// Launch helpers (all asynchronous on `st`).  Return hipError_t of the launch.
+hipError_t launch_prep_factors(const FactorSet& fs, const float* params, float beta, float thr,
+                               float* phi, float* dphi, const int32_t* stop, hipStream_t st);
+hipError_t launch_build_dense(const FactorSet& fs, const float* phi, const float* w, float* dense,
+                              const int32_t* stop, hipStream_t st);
+bool linear_fused_supported(int T, int CH);
+hipError_t launch_linear_fused(int T, int CH, int grid, const float* X, int64_t N, int64_t P,
+                               const float* B, const float* bias, const float* y, float scale,
+                               float* gpart, double* dpart, float* yhat, int64_t rows_per_wg,
+                               int reverse, const int32_t* stop, hipStream_t st);
+hipError_t prepare_linear_fused(int T, int CH, size_t lds_bytes, int* wg_per_cu);
+int rows_rb(int C);
+int cols_cw(int C);
+bool rows_supported(int C);
+hipError_t launch_rows(int C, int mode, int W, const float* X, int64_t N, int64_t P,
+                       const float* Bt, const float* bias, const void* target, const float* class_w,
+                       float scale, float* out, double* dpart, float* yhat, const int32_t* stop,
+                       hipStream_t st);
+int64_t rows_num_waves(int C, int64_t N);
+hipError_t launch_cols(int C, int W, int64_t nstripes, int64_t nchunks, const float* X, int64_t N,
+                       int64_t P, const float* V, int64_t rows_per_chunk, float* gpart, int reverse,
+                       const int32_t* stop, hipStream_t st);
+hipError_t launch_reduce_slabs(int W, const float* part, int64_t nslabs, int64_t ncols, float* out,
+                               const double* dpart, int64_t nd, double loss_scale, float* loss_slot,
+                               float* bias_slot, const int32_t* stop, hipStream_t st);
+hipError_t launch_mttkrp(const FactorSet& fs, const float* phi, const float* dphi, const float* w,
+                         const float* G, float* grad, const int32_t* stop, hipStream_t st);
+hipError_t launch_update(const FactorSet& fs, int has_bias, float* params, const float* grad,
+                         const UpdateArgs& ua, float* m, float* v, float* vmax, float* grad_total_out,
+                         float* loss_out, double* loss_hist, int32_t* stop, hipStream_t st);
+
+}  // namespace tr

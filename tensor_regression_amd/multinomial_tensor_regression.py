@@ -1,0 +1,354 @@
+"""CP multinomial logistic tensor regression on MI355X — drop-in for the reference's
+`multinomial_tensor_regression.py` (kimerein/tensor_regression).
+
+Same helpers, `model`, `CP_logistic_regression` class and semantics — including the
+reference's double softmax (the model returns probabilities and CrossEntropyLoss applies
+log-softmax to them again, multinomial_tensor_regression.py:180-187 + :448-450) — with the
+hot path (factor prep, X·B over all classes, softmax, weighted CE, X^T·dZ, MTTKRP, Adam)
+running as gfx950 HIP kernels through the C ABI.
+"""
+import numpy as np
+import torch
+
+from . import _engine, _lib
+from ._engine import Plan, as_device_f32, adam_hparams, run_adam_fit
+from .standard_tensor_regression import _plan_for, L2_penalty  # noqa: F401  (L2_penalty re-exported)
+
+__all__ = ["squeeze_integers", "confusion_matrix", "idx_to_oneHot", "make_BcpInit", "non_neg_fn", "model",
+           "L2_penalty", "CP_logistic_regression"]
+
+
+####################################
+######## Useful functions ##########
+####################################
+
+def squeeze_integers(intVec):
+    """Relabel integers to consecutive ids from 0 (multinomial…py:18-37)."""
+    intVec = np.asarray(intVec)
+    uniques = np.unique(intVec)
+    return np.searchsorted(uniques, intVec)
+
+
+def confusion_matrix(y_hat, y_true):
+    """Column-normalised confusion matrix (multinomial…py:45-65)."""
+    n_classes = np.max(y_true) + 1
+    if y_hat.ndim == 1:
+        y_hat = idx_to_oneHot(y_hat, n_classes)
+    cmat = y_hat.T @ idx_to_oneHot(y_true, n_classes)
+    return cmat / np.sum(cmat, axis=0)[None, :]
+
+
+def idx_to_oneHot(arr, n_classes=None):
+    """(multinomial…py:67-86)"""
+    if n_classes is None:
+        n_classes = np.max(arr) + 1
+    oneHot = np.zeros((arr.size, n_classes))
+    oneHot[np.arange(arr.size), arr] = 1
+    return oneHot
+
+
+def make_BcpInit(B_dims, rank, non_negative, scale=1, device='cpu'):
+    """Uniform init rand*scale - (1-nn)*scale/2, requires_grad (multinomial…py:88-114)."""
+    Bcp_init = [(torch.rand((B_dims[ii], rank)) * scale - (1 - non_negative[ii]) * (scale / 2)).to(device)
+                for ii in range(len(B_dims))]
+    for ii in range(len(B_dims)):
+        Bcp_init[ii].requires_grad = True
+    return Bcp_init
+
+
+def non_neg_fn(B_cp, non_negative, softplus_kwargs=None):
+    """(multinomial…py:116-146)"""
+    if softplus_kwargs is None:
+        softplus_kwargs = {'beta': 50, 'threshold': 1}
+    for ii in range(len(B_cp)):
+        if non_negative[ii]:
+            yield torch.nn.functional.softplus(B_cp[ii], **softplus_kwargs)
+        else:
+            yield B_cp[ii]
+
+
+def model(X, Bcp, weights, non_negative, softplus_kwargs=None):
+    """softmax(inner(X, cp_to_tensor((weights, non_neg_fn(Bcp))), n_modes=len(Bcp)-1), dim=1)
+    (multinomial_tensor_regression.py:148-187) on the gfx950 forward kernel; returns (N, C)."""
+    if not isinstance(X, torch.Tensor) or X.device.type != "cuda":
+        raise ValueError("model: X must be a torch tensor on a HIP device (device='cuda')")
+    K = len(Bcp) - 1
+    if X.ndim != K + 1 or list(X.shape[1:]) != [int(A.shape[0]) for A in Bcp[:-1]]:
+        raise ValueError(f"Incorrect shapes for inner product along {K} common modes. "
+                         f"tensor_1.shape={list(X.shape)}, factors={[tuple(A.shape) for A in Bcp]}")
+    dev = X.device
+    C, rank = int(Bcp[-1].shape[0]), int(Bcp[0].shape[1])
+    plan = _plan_for(_lib.TR_MODEL_MULTINOMIAL, X.shape[1:], C, rank, 1, non_negative, softplus_kwargs, dev)
+    arena = plan.pack([torch.as_tensor(A).to(dev) for A in Bcp])
+    w = torch.as_tensor(weights, dtype=torch.float32).to(dev).contiguous()
+    return plan.forward(as_device_f32(X, dev.index), arena, w)
+
+
+####################################
+########### Main class #############
+####################################
+
+class CP_logistic_regression():
+    def __init__(self, X, y, rank=5, non_negative=False, weights=None, Bcp_init=None, Bcp_init_scale=1,
+                 device='cpu', softplus_kwargs=None):
+        """(multinomial_tensor_regression.py:212-286; same arguments and attributes)."""
+        self.X = torch.as_tensor(X, dtype=torch.float32).to(device)
+        self.y = torch.as_tensor(y, dtype=torch.long).to(device)
+        if weights is None:
+            self.weights = torch.ones((rank), device=device)
+        else:
+            self.weights = torch.tensor(weights)
+        if softplus_kwargs is None:
+            self.softplus_kwargs = {'beta': 50, 'threshold': 1}
+        else:
+            self.softplus_kwargs = softplus_kwargs
+        self.rank = rank
+        self.device = device
+        if non_negative is True:
+            self.non_negative = [True] * (self.X.ndim)
+        elif non_negative is False:
+            self.non_negative = [False] * (self.X.ndim)
+        else:
+            self.non_negative = non_negative
+        self.n_classes = len(torch.unique(self.y))
+        B_dims = np.concatenate((np.array(self.X.shape[1:]), [self.n_classes]))
+        if Bcp_init is None:
+            self.Bcp = make_BcpInit(B_dims, self.rank, self.non_negative, scale=Bcp_init_scale, device=self.device)
+        else:
+            self.Bcp = Bcp_init
+        self.loss_running = []
+        self._plan = None
+        self._dev_cache = None
+
+    def return_self(self):
+        return self.Bcp
+
+    # ---- plumbing ------------------------------------------------------------------------------
+    def _device_data(self):
+        dev = _engine.compute_device(self.X, self.device)
+        c = self._dev_cache
+        if c is None or c[0] != dev or c[1] is not self.X or c[2] is not self.y:
+            Xd = as_device_f32(self.X, dev)
+            yd = self.y.to(f"cuda:{dev}", torch.long).contiguous()
+            C = int(self.Bcp[-1].shape[0])
+            ymin, ymax = int(yd.min().item()), int(yd.max().item())
+            if ymin < 0 or ymax >= C:
+                raise IndexError(f"Target {ymax if ymax >= C else ymin} is out of bounds.")
+            self._dev_cache = (dev, self.X, self.y, Xd, yd)
+        return self._dev_cache[0], self._dev_cache[3], self._dev_cache[4]
+
+    def _get_plan(self, Xd, rows):
+        dims = [int(A.shape[0]) for A in self.Bcp[:-1]]
+        if list(Xd.shape[1:]) != dims:
+            raise ValueError(f"Incorrect shapes for inner product along {len(dims)} common modes. "
+                             f"tensor_1.shape={list(Xd.shape)}, factors={[tuple(A.shape) for A in self.Bcp]}")
+        C, R = int(self.Bcp[-1].shape[0]), int(self.Bcp[0].shape[1])
+        p = self._plan
+        if p is None or p.max_rows < rows or p.feature_dims != dims or p.n_classes != C or p.rank != R:
+            p = Plan(_lib.TR_MODEL_MULTINOMIAL, dims, C, R, rows, self.non_negative, self.softplus_kwargs,
+                     Xd.device)
+            self._plan = p
+        return p
+
+    def _class_weights(self, weights, dev, yd, process_group=None):
+        cw = torch.as_tensor(weights, dtype=torch.float32).to(f"cuda:{dev}").contiguous()
+        C = int(self.Bcp[-1].shape[0])
+        if cw.ndim != 1 or cw.numel() != C:
+            raise RuntimeError(f"weight tensor should be defined either for all {C} classes or no classes "
+                               f"but got weight tensor of shape: {list(cw.shape)}")
+        W = cw.double()[yd].sum()
+        if process_group is not None:
+            import torch.distributed as dist
+            dist.all_reduce(W, group=process_group)
+        return cw, float(W.item())
+
+    # ---- fitting -------------------------------------------------------------------------------
+    def fit(self, lambda_L2=0.01, max_iter=1000, tol=1e-5, patience=10, weights=None, verbose=False,
+            running_loss_logging_interval=10, LBFGS_kwargs=None):
+        """LBFGS fit (multinomial_tensor_regression.py:291-387); closures evaluated on gfx950."""
+        if LBFGS_kwargs is None:
+            raise TypeError("torch.optim.lbfgs.LBFGS() argument after ** must be a mapping, not NoneType")
+        dev, Xd, yd = self._device_data()
+        plan = self._get_plan(Xd, Xd.shape[0])
+        cw, W = self._class_weights(weights, dev, yd)
+        optimizer = torch.optim.LBFGS(self.Bcp, **LBFGS_kwargs)
+        w = self.weights.to(f"cuda:{dev}", torch.float32).contiguous()
+        opts = dict(dtype=torch.float32, device=f"cuda:{dev}")
+        grad = torch.zeros(plan.num_grads, **opts)
+        gtot = torch.zeros(plan.num_params, **opts)
+        loss_out = torch.zeros(1, **opts)
+
+        def closure():
+            optimizer.zero_grad()
+            arena = plan.pack(self.Bcp)
+            plan.loss_grad(Xd, yd, cw, W, arena, w, grad)
+            plan.finalize_grad(arena, grad, lambda_L2, gtot, loss_out)
+            for A, g in zip(self.Bcp, plan.factor_views(gtot)):
+                A.grad = g.to(A.device).clone()
+            return loss_out[0].clone()
+
+        convergence_reached = False
+        for ii in range(max_iter):
+            if ii % running_loss_logging_interval == 0:
+                arena = plan.pack(self.Bcp)
+                plan.loss_grad(Xd, yd, cw, W, arena, w, grad)  # data loss only (reference :372)
+                self.loss_running.append(float(grad[-1].item()))
+                if verbose == 2:
+                    print(f'Iteration: {ii}, Loss: {self.loss_running[-1]}')
+            if ii > patience:
+                if np.sum(np.abs(np.diff(self.loss_running[ii - patience:]))) < tol:
+                    convergence_reached = True
+                    break
+            optimizer.step(closure)
+        if (verbose is True) or (verbose >= 1):
+            print('Convergence reached' if convergence_reached else
+                  'Reached maximum number of iterations without convergence')
+        return convergence_reached
+
+    def fit_Adam(self, lambda_L2=0.01, max_iter=1000, tol=1e-5, patience=10, weights=None, verbose=False,
+                 Adam_kwargs=None, process_group=None):
+        """Adam fit (multinomial_tensor_regression.py:389-471), device resident on gfx950.
+
+        process_group: optional torch.distributed group; self.X / self.y are then this rank's
+        sample shard (the CE normaliser sum_n w[y_n] is all-reduced once)."""
+        hp = adam_hparams(Adam_kwargs)
+        dev, Xd, yd = self._device_data()
+        plan = self._get_plan(Xd, Xd.shape[0])
+        cw, W = self._class_weights(weights, dev, yd, process_group)
+        allreduce = None
+        if process_group is not None:
+            import torch.distributed as dist
+
+            def allreduce(g):
+                dist.all_reduce(g, group=process_group)
+        arena = plan.pack(self.Bcp)
+        w = self.weights.to(f"cuda:{dev}", torch.float32).contiguous()
+        vcb = _Verbose() if verbose == 2 else None
+        convergence_reached, _ = run_adam_fit(plan, Xd, yd, cw, W, arena, w, lambda_L2, max_iter, tol, patience,
+                                              hp, self.loss_running, verbose_cb=vcb, allreduce=allreduce)
+        plan.unpack_into(arena, self.Bcp)
+        if (verbose is True) or (verbose >= 1):
+            print('Convergence reached' if convergence_reached else
+                  'Reached maximum number of iterations without convergence')
+        return convergence_reached
+
+    def predict(self, X=None, y_true=None, Bcp=None, device=None):
+        """(probabilities, argmax) as numpy (multinomial…py:474-545); the 'logit' the reference
+        returns is the softmax output (quirk Q2)."""
+        if device is None:
+            device = self.device
+        if X is None:
+            X = self.X
+        elif isinstance(X, torch.Tensor) is False:
+            X = torch.tensor(X, dtype=torch.float32, requires_grad=False).to(device)
+        elif X.device != torch.device(device):
+            X = X.to(device)
+        if Bcp is None:
+            Bcp = self.Bcp
+        elif isinstance(Bcp[0], torch.Tensor) is False:
+            for ii in range(len(Bcp)):
+                Bcp[ii] = torch.tensor(Bcp[ii], dtype=torch.float32, requires_grad=False).to(device)
+        elif Bcp[0].device != torch.device(device):
+            for ii in range(len(Bcp)):
+                Bcp[ii] = Bcp[ii].to(device)
+        dev = _engine.compute_device(X, device)
+        Xd = as_device_f32(X, dev)
+        logit = model(Xd, [torch.as_tensor(A).to(f"cuda:{dev}") for A in Bcp], self.weights, self.non_negative,
+                      softplus_kwargs=self.softplus_kwargs).detach().cpu().numpy()
+        pred = np.argmax(logit, axis=1)
+        return logit, pred
+
+    def return_Bcp_final(self):
+        Bcp = list(non_neg_fn(self.Bcp, self.non_negative, softplus_kwargs=self.softplus_kwargs))
+        return [Bcp[ii].detach().cpu().numpy() for ii in range(len(Bcp))]
+
+    def make_confusion_matrix(self, prob_or_pred='pred', prob=None, pred=None, y_true=None):
+        """(multinomial…py:562-597)"""
+        if (prob is None) and (pred is None):
+            prob, pred = self.predict()
+        if y_true is None:
+            y_true = self.y.detach().cpu().numpy()
+        if prob_or_pred == 'pred':
+            cm = confusion_matrix(pred, y_true)
+        elif prob_or_pred == 'prob':
+            cm = confusion_matrix(prob, y_true)
+        acc = np.sum(np.diag(cm)) / np.sum(cm)
+        return cm, acc
+
+    def detach_Bcp(self):
+        return [Bcp.detach().cpu().numpy() for Bcp in self.Bcp]
+
+    def get_params(self):
+        # the reference reads a nonexistent self.bias here (quirk Q4); the working subset is returned
+        return {'X': self.X.detach().cpu().numpy(),
+                'y': self.y.detach().cpu().numpy(),
+                'weights': self.weights.detach().cpu().numpy(),
+                'Bcp': self.detach_Bcp(),
+                'non_negative': self.non_negative,
+                'softplus_kwargs': self.softplus_kwargs,
+                'rank': self.rank,
+                'device': self.device,
+                'loss_running': self.loss_running}
+
+    def set_params(self, params):
+        self.X = params['X']
+        self.y = params['y']
+        self.weights = params['weights']
+        self.Bcp = params['Bcp']
+        if 'bias' in params:
+            self.bias = params['bias']
+        self.non_negative = params['non_negative']
+        self.softplus_kwargs = params['softplus_kwargs']
+        self.rank = params['rank']
+        self.device = params['device']
+        self.loss_running = params['loss_running']
+        self._plan = None
+        self._dev_cache = None
+
+    def display_params(self):
+        print('X:', self.X.shape)
+        print('y:', self.y.shape)
+        print('weights:', self.weights)
+        print('Bcp:', self.Bcp)
+        print('non_negative:', self.non_negative)
+        print('softplus_kwargs:', self.softplus_kwargs)
+        print('rank:', self.rank)
+        print('device:', self.device)
+        print('loss_running:', self.loss_running)
+
+    def plot_outputs(self):
+        import matplotlib.pyplot as plt
+        plt.figure()
+        plt.plot(self.loss_running)
+        plt.xlabel('logged iteration')
+        plt.ylabel('loss')
+        plt.title('loss')
+        logit, pred = self.predict()
+        fig, axs = plt.subplots(2)
+        axs[0].imshow(idx_to_oneHot(pred, self.n_classes), aspect='auto', interpolation='none')
+        axs[1].imshow(idx_to_oneHot(self.y.detach().cpu().numpy(), self.n_classes), aspect='auto',
+                      interpolation='none')
+        axs[1].set_xlabel('class')
+        fig.suptitle('predictions')
+        cm, acc = self.make_confusion_matrix(prob_or_pred='pred')
+        fig = plt.figure()
+        plt.imshow(cm)
+        plt.ylabel('true class')
+        plt.xlabel('predicted class')
+        plt.title('confusion matrix (predictions)')
+        Bcp_final = self.return_Bcp_final()
+        fig, axs = plt.subplots(len(Bcp_final))
+        for ii, val in enumerate(Bcp_final):
+            axs[ii].set_title(f'factor {ii}')
+            axs[ii].plot(val)
+        fig.suptitle('components')
+
+
+class _Verbose:
+    """verbose==2 print of the multinomial fit_Adam (multinomial…py:460-461)."""
+
+    def before_step(self, arena):
+        pass
+
+    def after_step(self, ii, loss):
+        print(f'Iteration: {ii}, Loss: {loss}')

@@ -1,0 +1,49 @@
+"""Loader for the golden fixtures in tests/golden (generated from the reference by tools/gen_golden.py)."""
+import json
+import os
+
+import numpy as np
+import torch
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def names(prefix=""):
+    out = []
+    for f in sorted(os.listdir(GOLDEN)):
+        if f.endswith(".npz") and f.startswith(prefix) and not f.startswith("init_"):
+            out.append(f[:-4])
+    return out
+
+
+def split(flat, shapes):
+    out, k = [], 0
+    for s in shapes:
+        n = int(np.prod(s))
+        out.append(np.asarray(flat[k:k + n], dtype=np.float32).reshape(s))
+        k += n
+    return out
+
+
+def load(name):
+    d = dict(np.load(os.path.join(GOLDEN, name + ".npz")))
+    meta = json.loads(str(d.pop("meta")))
+    shapes = [tuple(s) for s in meta["factor_shapes"]]
+    d["X"] = torch.tensor(d["X_q"].astype(np.float32) / 8.0)
+    d["Bcp0_list"] = split(d["Bcp0"], shapes)
+    if "Bcp_final" in d:
+        d["Bcp_final_list"] = split(d["Bcp_final"], shapes)
+    if "grads0" in d:
+        d["grads0_list"] = split(d["grads0"], shapes)
+    if "Bcp_final2" in d:
+        d["Bcp_final2_list"] = split(d["Bcp_final2"], shapes)
+    d["meta"] = meta
+    d["shapes"] = shapes
+    return d
+
+
+def normwise_rel(a, b):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    den = np.linalg.norm(b.ravel())
+    return float(np.linalg.norm((a - b).ravel()) / (den if den > 0 else 1.0))

@@ -1,0 +1,216 @@
+#!/usr/bin/env python3
+"""Generate golden fixtures by running the REFERENCE itself (build container only).
+
+    PYTHONDONTWRITEBYTECODE=1 python tools/gen_golden.py [--kat]
+
+Imports kimerein/tensor_regression from /root/reference (read-only) with the tensorly stand-in
+of oracle/tensorly_standin on sys.path, runs small seeded cases through the reference's own
+classes and functions, and writes inputs + outputs to tests/golden/*.npz (data only: nothing
+of the reference's source travels).  Inputs are exactly representable (X = int8 / 8), so the
+fixtures stay small and any consumer reconstructs bit-identical fp32 inputs.
+
+--kat additionally replays the two notebook known-answer traces (KAT-1: LBFGS fp64,
+demo_TensorRegression.ipynb; KAT-2: Adam-amsgrad fp32, demo_MultinomialTensorRegression.ipynb)
+through the reference + stand-in and records the agreement in tests/golden/kat_replay.json.
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF = "/root/reference"
+sys.path.insert(0, os.path.join(REPO, "oracle", "tensorly_standin"))
+sys.path.insert(0, REF)
+sys.dont_write_bytecode = True
+
+import standard_tensor_regression as STR  # noqa: E402  (reference)
+import multinomial_tensor_regression as MTR  # noqa: E402  (reference)
+
+OUT = os.path.join(REPO, "tests", "golden")
+
+
+def exact_X(rng, shape):
+    q = rng.integers(-8, 9, size=shape).astype(np.int8)
+    return q, torch.tensor(q.astype(np.float32) / 8.0)
+
+
+def save(name, **arrays):
+    path = os.path.join(OUT, name + ".npz")
+    np.savez_compressed(path, **arrays)
+    print("wrote", path, os.path.getsize(path), "bytes")
+
+
+def linear_case(name, seed, shape, rank, non_negative, bias_init, lam, adam_kwargs, iters, tol=0.0, patience=10,
+                softplus=None, second_fit=0):
+    rng = np.random.default_rng(seed)
+    Xq, X = exact_X(rng, shape)
+    y = torch.tensor(rng.standard_normal(shape[0]).astype(np.float32))
+    torch.manual_seed(seed)
+    m = STR.CP_linear_regression(X.shape, rank=rank, non_negative=non_negative, bias_init=bias_init,
+                                 softplus_kwargs=softplus)
+    Bcp0 = [A.detach().numpy().copy() for A in m.Bcp]
+    b0 = m.bias.detach().numpy().copy()
+    # one forward + loss + backward at the initial point (standard…py:459-462)
+    y_hat = STR.lin_model(X, m.Bcp, m.weights, m.non_negative, m.bias, softplus_kwargs=m.softplus_kwargs)
+    loss = torch.nn.MSELoss()(y_hat, y) + lam * STR.L2_penalty(m.Bcp)
+    loss.backward()
+    grads = [A.grad.numpy().copy() for A in m.Bcp]
+    bgrad = m.bias.grad.numpy().copy()
+    for A in m.Bcp:
+        A.grad = None
+    m.bias.grad = None
+    conv = m.fit_Adam(X, y, lambda_L2=lam, max_iter=iters, tol=tol, patience=patience, verbose=False,
+                      Adam_kwargs=dict(adam_kwargs))
+    out = dict(X_q=Xq, y=y.numpy(), Bcp0=np.array(Bcp0, dtype=object) if False else np.concatenate(
+        [a.reshape(-1) for a in Bcp0]), bias0=b0, y_hat0=y_hat.detach().numpy(), loss0=np.float64(loss.item()),
+        grads0=np.concatenate([g.reshape(-1) for g in grads]), bias_grad0=bgrad,
+        loss_running=np.array(m.loss_running, dtype=np.float64),
+        Bcp_final=np.concatenate([A.detach().numpy().reshape(-1) for A in m.Bcp]),
+        bias_final=m.bias.detach().numpy().copy(), converged=np.int32(conv))
+    if second_fit:
+        m.fit_Adam(X, y, lambda_L2=lam, max_iter=second_fit, tol=tol, patience=patience, verbose=False,
+                   Adam_kwargs=dict(adam_kwargs))
+        out.update(loss_running2=np.array(m.loss_running, dtype=np.float64),
+                   Bcp_final2=np.concatenate([A.detach().numpy().reshape(-1) for A in m.Bcp]),
+                   bias_final2=m.bias.detach().numpy().copy())
+    meta = dict(model="linear", seed=seed, shape=list(shape), rank=rank, non_negative=list(map(bool, non_negative)),
+                bias_init=bias_init, lambda_L2=lam, adam_kwargs=adam_kwargs, max_iter=iters, tol=tol,
+                patience=patience, softplus_kwargs=m.softplus_kwargs, second_fit=second_fit,
+                factor_shapes=[list(a.shape) for a in Bcp0], torch=torch.__version__)
+    out["meta"] = np.array(json.dumps(meta))
+    save(name, **out)
+
+
+def linear_lbfgs_case(name, seed, shape, rank, lam, iters, lbfgs_kwargs, logging_interval=1):
+    rng = np.random.default_rng(seed)
+    Xq, X = exact_X(rng, shape)
+    y = torch.tensor(rng.standard_normal(shape[0]).astype(np.float32))
+    torch.manual_seed(seed)
+    m = STR.CP_linear_regression(X.shape, rank=rank)
+    Bcp0 = [A.detach().numpy().copy() for A in m.Bcp]
+    conv = m.fit(X, y, lambda_L2=lam, max_iter=iters, tol=0.0, patience=100, verbose=False,
+                 running_loss_logging_interval=logging_interval, LBFGS_kwargs=dict(lbfgs_kwargs))
+    meta = dict(model="linear_lbfgs", seed=seed, shape=list(shape), rank=rank, lambda_L2=lam, max_iter=iters,
+                lbfgs_kwargs=lbfgs_kwargs, logging_interval=logging_interval,
+                factor_shapes=[list(a.shape) for a in Bcp0], torch=torch.__version__)
+    save(name, X_q=Xq, y=y.numpy(), Bcp0=np.concatenate([a.reshape(-1) for a in Bcp0]),
+         loss_running=np.array(m.loss_running), Bcp_final=np.concatenate(
+             [A.detach().numpy().reshape(-1) for A in m.Bcp]), bias_final=m.bias.detach().numpy(),
+         converged=np.int32(conv), meta=np.array(json.dumps(meta)))
+
+
+def mnl_case(name, seed, shape, n_classes, rank, non_negative, class_w, lam, adam_kwargs, iters, tol=0.0,
+             patience=10):
+    rng = np.random.default_rng(seed)
+    Xq, X = exact_X(rng, shape)
+    y = rng.integers(0, n_classes, size=shape[0])
+    y[:n_classes] = np.arange(n_classes)  # every class present (n_classes = len(unique(y)))
+    torch.manual_seed(seed)
+    m = MTR.CP_logistic_regression(X.numpy(), y, rank=rank, non_negative=non_negative)
+    Bcp0 = [A.detach().numpy().copy() for A in m.Bcp]
+    S = MTR.model(m.X, m.Bcp, m.weights, m.non_negative, softplus_kwargs=m.softplus_kwargs)
+    loss_fn = torch.nn.CrossEntropyLoss(weight=torch.as_tensor(class_w, dtype=torch.float32))
+    loss = loss_fn(S, m.y) + lam * MTR.L2_penalty(m.Bcp)
+    loss.backward()
+    grads = [A.grad.numpy().copy() for A in m.Bcp]
+    for A in m.Bcp:
+        A.grad = None
+    conv = m.fit_Adam(lambda_L2=lam, max_iter=iters, tol=tol, patience=patience, weights=np.asarray(class_w),
+                      verbose=False, Adam_kwargs=dict(adam_kwargs))
+    meta = dict(model="multinomial", seed=seed, shape=list(shape), n_classes=n_classes, rank=rank,
+                non_negative=list(map(bool, non_negative)), class_weights=list(map(float, class_w)), lambda_L2=lam,
+                adam_kwargs=adam_kwargs, max_iter=iters, tol=tol, patience=patience,
+                softplus_kwargs=m.softplus_kwargs, factor_shapes=[list(a.shape) for a in Bcp0],
+                torch=torch.__version__)
+    save(name, X_q=Xq, y=y.astype(np.int64), Bcp0=np.concatenate([a.reshape(-1) for a in Bcp0]),
+         probs0=S.detach().numpy(), loss0=np.float64(loss.item()),
+         grads0=np.concatenate([g.reshape(-1) for g in grads]),
+         loss_running=np.array(m.loss_running, dtype=np.float64),
+         Bcp_final=np.concatenate([A.detach().numpy().reshape(-1) for A in m.Bcp]), converged=np.int32(conv),
+         meta=np.array(json.dumps(meta)))
+
+
+def init_case(name):
+    """make_BcpInit RNG parity: the reference's initialisers for fixed seeds."""
+    out = {}
+    for seed, dims, rank, nn, scale in [(0, [7, 5], 3, [False, False], 1.0), (1, [6, 4, 3], 2, [True, False, True], 0.5),
+                                        (2, [1, 9], 2, [True, True], 1.0)]:
+        torch.manual_seed(seed)
+        B = STR.make_BcpInit(dims, rank, nn, scale=scale)
+        out[f"std_{seed}"] = np.concatenate([b.numpy().reshape(-1) for b in B])
+        torch.manual_seed(seed)
+        M = MTR.make_BcpInit(dims, rank, nn, scale=scale)
+        out[f"mnl_{seed}"] = np.concatenate([b.detach().numpy().reshape(-1) for b in M])
+    save(name, **out)
+
+
+def kat_replay():
+    import scipy.signal
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from kat_data import kat_inputs, KAT1_TRACE, KAT2_TRACE  # noqa: E402
+    res = {}
+    # KAT-2 (multinomial, Adam amsgrad, fp32): notebook cells 2/4, one extra make_BcpInit draw
+    X, y = kat_inputs("kat2")
+    MTR.make_BcpInit(np.concatenate((X.shape[1:], [5])), 4, [False] * 3, scale=1)
+    m = MTR.CP_logistic_regression(X, y, rank=4, non_negative=[False] * 3, Bcp_init_scale=1,
+                                   softplus_kwargs={'beta': 50, 'threshold': 1})
+    m.fit_Adam(lambda_L2=0.01, max_iter=len(KAT2_TRACE), tol=1e-6, patience=100, weights=np.ones(5),
+               Adam_kwargs={'lr': 0.01, 'amsgrad': True})
+    rel = np.max(np.abs(np.array(m.loss_running) - KAT2_TRACE) / np.abs(KAT2_TRACE))
+    res["kat2_max_rel"] = float(rel)
+    res["kat2_loss_running"] = m.loss_running
+    del m, X
+    # KAT-1 (linear, LBFGS, fp64)
+    X, y = kat_inputs("kat1")
+    m = STR.CP_linear_regression(X.shape, dtype=X.dtype, rank=10, non_negative=[False, False], Bcp_init_scale=0.005,
+                                 softplus_kwargs={'beta': 50, 'threshold': 1})
+    m.fit(X, y, lambda_L2=1e-5, max_iter=200, tol=1e-50, patience=10, running_loss_logging_interval=1,
+          LBFGS_kwargs={'lr': 1, 'max_iter': 20, 'max_eval': None, 'tolerance_grad': 1e-07,
+                        'tolerance_change': 1e-09, 'history_size': 100, 'line_search_fn': "strong_wolfe"})
+    n = min(len(m.loss_running), len(KAT1_TRACE))
+    rel = np.max(np.abs(np.array(m.loss_running[:n]) - KAT1_TRACE[:n]) / np.abs(KAT1_TRACE[:n]))
+    res["kat1_max_rel"] = float(rel)
+    res["kat1_len"] = len(m.loss_running)
+    res["kat1_loss_running"] = m.loss_running
+    with open(os.path.join(OUT, "kat_replay.json"), "w") as f:
+        json.dump(res, f, indent=1)
+    print("KAT replay:", {k: v for k, v in res.items() if "rel" in k or "len" in k})
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--kat", action="store_true")
+    args = ap.parse_args()
+    os.makedirs(OUT, exist_ok=True)
+    torch.set_num_threads(1)  # fixed summation order for the golden outputs
+    adam = {'lr': 0.01}
+    linear_case("lin_basic", 11, (64, 8, 4), 2, [False, False, False], 0.3, 0.01, adam, 50)
+    linear_case("lin_nonneg_amsgrad_wd", 12, (96, 12, 8), 3, [True, False, True], -0.2, 0.05,
+                {'lr': 0.02, 'amsgrad': True, 'weight_decay': 0.01, 'betas': (0.8, 0.99), 'eps': 1e-6}, 50)
+    linear_case("lin_4d_unaligned", 13, (40, 4, 3, 5), 4, [False, True, False, False], 0.0, 0.01, adam, 50)
+    linear_case("lin_fused_shape", 14, (256, 16, 16), 8, [False, False, False], 0.1, 0.01, adam, 50)
+    linear_case("lin_one_mode", 15, (64, 40), 2, [False, False], 0.0, 0.01, adam, 30)
+    linear_case("lin_converge", 16, (64, 8, 4), 2, [False, False, False], 0.0, 0.01, {'lr': 0.001}, 400,
+                tol=0.05, patience=5, second_fit=30)
+    linear_case("lin_softplus_kw", 17, (48, 6, 4), 2, [True, True, False], 0.0, 0.01, adam, 30,
+                softplus={'beta': 5, 'threshold': 2})
+    linear_lbfgs_case("lin_lbfgs", 18, (64, 8, 4), 2, 1e-3, 6,
+                      {'lr': 1, 'max_iter': 20, 'max_eval': None, 'tolerance_grad': 1e-07,
+                       'tolerance_change': 1e-09, 'history_size': 100, 'line_search_fn': "strong_wolfe"})
+    mnl_case("mnl_basic", 21, (128, 8, 4), 3, 2, [False, False, False], [1, 1, 1], 0.01, adam, 50)
+    mnl_case("mnl_nonneg_weighted_amsgrad", 22, (160, 6, 5), 4, 3, [True, False, True], [0.5, 2.0, 1.0, 1.5], 0.02,
+             {'lr': 0.01, 'amsgrad': True}, 50)
+    mnl_case("mnl_c10", 23, (256, 16, 8), 10, 4, [False, False, False], [1.0] * 10, 0.01, adam, 50)
+    mnl_case("mnl_converge", 24, (96, 4, 4), 2, 2, [False, False, False], [1, 1], 0.01, {'lr': 0.001}, 300,
+             tol=0.01, patience=5)
+    init_case("init_rng")
+    if args.kat:
+        kat_replay()
+
+
+if __name__ == "__main__":
+    main()
