@@ -1,0 +1,238 @@
+#!/usr/bin/env python3
+"""Benchmark: CP tensor-regression fit_Adam iterations on MI355X (gfx950 HIP path).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4] [--no-cpu-baseline]
+    torchrun --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N ...   (N > 1)
+
+A "step" is one fit_Adam iteration of the reference (standard_tensor_regression.py:458-470):
+forward + MSE (+L2) + gradient + Adam over every sample the rank holds.  Default workload =
+BASELINE.json configs[1]: X (65536, 256, 128) fp32 per GPU, rank 8 (weak scaling: every rank
+holds its own 65536-sample shard; one RCCL all-reduce of the gradient arena per step).
+Inputs are synthetic (seeded torch.randn on the device; planted rank-8 model + noise) and are
+resident in HBM before the timed region.  `value` = samples processed by all ranks / max-over-
+ranks wall time of the K timed steps.
+
+roofline: the dominant kernel (the single-pass X stream, k_linear_fused) timed with hipEvents on
+its own stream during the timed region; algorithmic bytes per launch = N*P*4 (X read once) +
+N*4 (y).  cpu_baseline: the oracle (a torch-CPU restatement of the reference's op sequence,
+oracle/cp_oracle.py) timed on this host on the same X for a bounded number of iterations.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+METRIC = "training samples/sec + achieved HBM GB/s, 3-D CP regression rank=8, 1/2/4/8 MI355X"
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+CONFIGS = {
+    "c2": dict(kind="linear", rows=65536, dims=(256, 128), rank=8,
+               workload="configs[1]: 3-D standard CP regression, X (65536, 256, 128) fp32 per GPU, rank 8, "
+                        "MSE + L2 (lambda 0.01), Adam lr 0.01"),
+    "c3": dict(kind="multinomial", rows=65536, dims=(128, 64), rank=8, classes=10,
+               workload="configs[2]: multinomial CP regression, X (65536, 128, 64) fp32 per GPU, 10 classes, "
+                        "rank 8, softmax + weighted CE + L2, Adam lr 0.01"),
+    "c4": dict(kind="linear", rows=16384, dims=(64, 64, 32), rank=16,
+               workload="configs[3]: 4-D CP regression, X (131072, 64, 64, 32) sharded 16384 samples per GPU, "
+                        "rank 16, Adam lr 0.01"),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def make_data(cfg, rank_id, dev):
+    """Seeded synthetic shard for this rank: X ~ N(0,1), planted CP model, y / labels."""
+    g = torch.Generator(device=dev).manual_seed(1234 + rank_id)
+    N, dims, R = cfg["rows"], cfg["dims"], cfg["rank"]
+    X = torch.randn((N,) + tuple(dims), device=dev, generator=g, dtype=torch.float32)
+    gc = torch.Generator().manual_seed(99)  # planted factors identical on every rank
+    if cfg["kind"] == "linear":
+        from tensor_regression_amd.standard_tensor_regression import lin_model
+        A = [(torch.randn(d, R, generator=gc) / 4).to(dev) for d in dims]
+        y = lin_model(X, A, torch.ones(R, device=dev), [False] * len(A), torch.zeros(1, device=dev))
+        y = y + 0.1 * torch.randn(N, device=dev, generator=g)
+        return X, y
+    from tensor_regression_amd.multinomial_tensor_regression import model as mnl_model
+    C = cfg["classes"]
+    A = [(torch.randn(d, R, generator=gc) / 3).to(dev) for d in dims] + [torch.randn(C, R, generator=gc).to(dev)]
+    S = mnl_model(X, A, torch.ones(R, device=dev), [False] * len(A))
+    y = torch.multinomial(S, 1, generator=g).reshape(-1)
+    y[:C] = torch.arange(C, device=dev)
+    return X, y
+
+
+def cpu_baseline(cfg, X, y, model_init, budget_s=15.0):
+    """Oracle (reference op sequence on torch CPU) on the same X: bounded iterations."""
+    from oracle import cp_oracle
+    Xc = X.cpu()
+    yc = y.cpu()
+    R = cfg["rank"]
+    t_copy = time.perf_counter()
+    lam, adam = 0.01, {"lr": 0.01}
+
+    def run(iters):
+        if cfg["kind"] == "linear":
+            return cp_oracle.fit_adam_linear(Xc, yc, model_init[0], model_init[1], np.ones(R, np.float32),
+                                             [False] * len(cfg["dims"]), lam, iters, 0.0, 10, adam)
+        return cp_oracle.fit_adam_mnl(Xc, yc, model_init[0], np.ones(R, np.float32),
+                                      [False] * (len(cfg["dims"]) + 1), np.ones(cfg["classes"], np.float32), lam,
+                                      iters, 0.0, 10, adam)
+
+    t0 = time.perf_counter()
+    run(1)  # warm-up (allocator, thread pool)
+    t1 = time.perf_counter()
+    per = max(t1 - t0, 1e-3)
+    iters = int(max(2, min(200, budget_s / per)))
+    t0 = time.perf_counter()
+    run(iters)
+    el = time.perf_counter() - t0
+    N = X.shape[0]
+    return {"value": N * iters / el, "unit": "samples/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"oracle/cp_oracle.py fit_Adam (torch {torch.__version__} CPU, reference op order) on the "
+                      f"same {N} x {list(cfg['dims'])} X, {iters} timed iterations after 1 warm-up "
+                      f"({el:.1f} s); os.cpu_count()={os.cpu_count()}",
+            "ms_per_step": 1e3 * el / iters}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--traffic", default=os.path.join(HERE, "profiles", "traffic.json"),
+                    help="PMC traffic summary (tools/pmc_traffic.py output) for the roofline 'traffic' field")
+    args = ap.parse_args()
+    cfg = CONFIGS[args.config]
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank_id = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    pg = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        pg = dist.group.WORLD
+    dev = f"cuda:{local}"
+    torch.cuda.set_device(local)
+
+    from tensor_regression_amd import CP_linear_regression, CP_logistic_regression
+
+    X, y = make_data(cfg, rank_id, dev)
+    torch.cuda.synchronize()
+    R = cfg["rank"]
+    torch.manual_seed(1)
+    if cfg["kind"] == "linear":
+        model = CP_linear_regression(X.shape, rank=R, device=dev)
+        init = ([a.detach().cpu().numpy().copy() for a in model.Bcp], model.bias.detach().cpu().numpy().copy())
+
+        def fit(iters):
+            return model.fit_Adam(X, y, lambda_L2=0.01, max_iter=iters, tol=0, patience=10,
+                                  Adam_kwargs={"lr": 0.01}, process_group=pg)
+    else:
+        model = CP_logistic_regression(X, y, rank=R, device=dev)
+        init = ([a.detach().cpu().numpy().copy() for a in model.Bcp], None)
+        cw = np.ones(cfg["classes"], np.float32)
+
+        def fit(iters):
+            return model.fit_Adam(lambda_L2=0.01, max_iter=iters, tol=0, patience=10, weights=cw,
+                                  Adam_kwargs={"lr": 0.01}, process_group=pg)
+
+    fit(args.warmup)
+    plan = model._plan
+    plan.read_timing()
+    plan.set_timing(True)
+
+    def barrier():
+        if pg is not None:
+            torch.distributed.barrier()
+
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    fit(args.steps)
+    torch.cuda.synchronize()
+    barrier()
+    el = time.perf_counter() - t0
+    plan.set_timing(False)
+    kt = plan.read_timing()
+    if pg is not None:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        el = float(t.item())
+    N = X.shape[0]
+    P = int(np.prod(cfg["dims"]))
+    ms_step = 1e3 * el / args.steps
+    value = world * N * args.steps / el
+
+    stream_kinds = ["stream_fused"] if kt["stream_fused"][1] else ["stream_rows", "stream_cols"]
+    kernel_avg = {k: (v[0] / v[1] if v[1] else None) for k, v in kt.items()}
+    if kt["stream_fused"][1]:
+        dom = "stream_fused"
+        bytes_launch = N * P * 4 + N * 4
+        dom_name = "k_linear_fused"
+    else:
+        dom = "stream_rows" if kt["stream_rows"][0] >= kt["stream_cols"][0] else "stream_cols"
+        bytes_launch = N * P * 4 + N * 4 * (cfg.get("classes", 1))
+        dom_name = "k_rows" if dom == "stream_rows" else "k_cols"
+    dom_ms = kernel_avg[dom]
+    achieved = bytes_launch / (dom_ms * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(args.traffic):
+        try:
+            with open(args.traffic) as f:
+                tj = json.load(f)
+            ent = tj.get(args.config, {}).get(dom_name)
+            if ent:
+                traffic = ent.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    iter_bytes = sum(N * P * 4 for _ in stream_kinds)
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "samples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (seeded torch.randn X on device, planted CP model + noise)",
+        "config": {"workload": cfg["workload"], "samples_per_gpu": N, "feature_dims": list(cfg["dims"]),
+                   "rank": R, "global_batch": world * N,
+                   "parallelism": f"dp{world} sample-sharded, one RCCL all-reduce of the gradient arena per step",
+                   "plan": plan.describe},
+        "achieved_hbm_GBps_per_gpu": iter_bytes / (ms_step * 1e-3) / 1e9,
+        "roofline": {"bound": "hbm", "kernel": dom_name, "achieved": achieved, "peak": HBM_PEAK_GBPS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
+                     "kernel_avg_ms": dom_ms, "algorithmic_bytes_per_launch": bytes_launch},
+        "kernel_avg_ms": kernel_avg,
+    }
+    if rank_id == 0 and world == 1 and not args.no_cpu_baseline:
+        log("cpu baseline ...")
+        out["cpu_baseline"] = cpu_baseline(cfg, X, y, init, args.cpu_budget)
+    else:
+        out["cpu_baseline"] = None
+    if rank_id == 0:
+        print(json.dumps(out), flush=True)
+    if pg is not None:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

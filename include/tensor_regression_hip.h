@@ -149,6 +149,25 @@ int tr_adam_step(tr_plan* plan, float* params, const float* grad, float* exp_avg
                  int64_t step, double* loss_hist, int64_t hist_base, int64_t iter,
                  int64_t patience, double tol, int32_t* stop_flag, void* stream);
 
+/*
+ * Per-kernel device timing (measurement support; no reference counterpart).
+ * When enabled, every launch of the plan is bracketed by hipEvents on the caller's stream
+ * (no host synchronisation).  tr_plan_read_timing synchronises the recorded events and returns,
+ * per kernel kind (TR_KERNEL_*), the summed elapsed milliseconds and the number of launches,
+ * then clears the record.
+ */
+#define TR_KERNEL_STREAM_FUSED 0 /* single-pass X stream (linear) */
+#define TR_KERNEL_STREAM_ROWS 1  /* two-pass forward X stream */
+#define TR_KERNEL_STREAM_COLS 2  /* two-pass backward X stream */
+#define TR_KERNEL_REDUCE 3       /* slab reduction */
+#define TR_KERNEL_MTTKRP 4       /* factor gradients */
+#define TR_KERNEL_PREP 5         /* softplus + dense B */
+#define TR_KERNEL_UPDATE 6       /* L2 + Adam + plateau test */
+#define TR_KERNEL_NKINDS 7
+int tr_plan_set_timing(tr_plan* plan, int enable);
+int tr_plan_read_timing(tr_plan* plan, double* total_ms /* [TR_KERNEL_NKINDS] */,
+                        int64_t* launches /* [TR_KERNEL_NKINDS] */);
+
 #ifdef __cplusplus
 }
 #endif

@@ -158,6 +158,18 @@ class Plan:
         return [arena[self.offsets[f]:self.offsets[f + 1]].view(shp)
                 for f, shp in enumerate(self.factor_shapes())]
 
+    # ---- timing ------------------------------------------------------------------------------
+    def set_timing(self, enable):
+        check(self.lib.tr_plan_set_timing(self.h, 1 if enable else 0), "tr_plan_set_timing")
+
+    def read_timing(self):
+        """{kernel kind: (total_ms, launches)} since the last read (synchronises the events)."""
+        n = len(_lib.KERNEL_KINDS)
+        ms = (ctypes.c_double * n)()
+        cnt = (ctypes.c_int64 * n)()
+        check(self.lib.tr_plan_read_timing(self.h, ms, cnt), "tr_plan_read_timing")
+        return {k: (ms[i], cnt[i]) for i, k in enumerate(_lib.KERNEL_KINDS)}
+
     # ---- entry points ------------------------------------------------------------------------
     def forward(self, X, arena, weights, out=None):
         N = X.shape[0]

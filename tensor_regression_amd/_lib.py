@@ -16,6 +16,7 @@ TR_ABI_VERSION = 1
 TR_MODEL_LINEAR = 0
 TR_MODEL_MULTINOMIAL = 1
 TR_MAX_FACTORS = 8
+KERNEL_KINDS = ["stream_fused", "stream_rows", "stream_cols", "reduce", "mttkrp", "prep", "update"]
 
 # exported symbol -> (restype, argtypes)
 _c = ctypes
@@ -35,6 +36,8 @@ SIGNATURES = {
     "tr_forward": (_c.c_int, [_vp, _vp, _c.c_int64, _vp, _vp, _vp, _vp]),
     "tr_loss_grad": (_c.c_int, [_vp, _vp, _c.c_int64, _vp, _vp, _c.c_double, _vp, _vp, _vp, _vp, _vp, _vp]),
     "tr_finalize_grad": (_c.c_int, [_vp, _vp, _vp, _c.c_float, _vp, _vp, _vp]),
+    "tr_plan_set_timing": (_c.c_int, [_vp, _c.c_int]),
+    "tr_plan_read_timing": (_c.c_int, [_vp, _c.POINTER(_c.c_double), _c.POINTER(_c.c_int64)]),
     "tr_adam_step": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _c.c_float, _c.c_double, _c.c_double,
                                 _c.c_double, _c.c_double, _c.c_double, _c.c_int, _c.c_int64, _vp,
                                 _c.c_int64, _c.c_int64, _c.c_int64, _c.c_double, _vp, _vp]),

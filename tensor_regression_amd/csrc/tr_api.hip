@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "../../include/tensor_regression_hip.h"
 #include "tr_kernels.h"
@@ -42,6 +43,50 @@ struct tr_plan {
   int64_t gpart_slabs = 0, dpart_n = 0;
   unsigned parity = 0;
   std::string desc;
+  // optional per-kernel event timing (tr_plan_set_timing)
+  int timing = 0;
+  struct Rec {
+    hipEvent_t a, b;
+    int kind;
+  };
+  std::vector<Rec> recs;
+  std::vector<hipEvent_t> pool;
+};
+
+static hipEvent_t take_event(tr_plan* p) {
+  if (!p->pool.empty()) {
+    hipEvent_t e = p->pool.back();
+    p->pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+// Brackets one kernel launch with events when timing is on (no host synchronisation).
+struct TimedLaunch {
+  tr_plan* p;
+  hipStream_t st;
+  int kind;
+  hipEvent_t a = nullptr;
+  TimedLaunch(tr_plan* p_, hipStream_t st_, int kind_) : p(p_), st(st_), kind(kind_) {
+    if (p->timing) {
+      a = take_event(p);
+      if (a) (void)hipEventRecord(a, st);
+    }
+  }
+  ~TimedLaunch() {
+    if (a) {
+      hipEvent_t b = take_event(p);
+      if (b) {
+        (void)hipEventRecord(b, st);
+        p->recs.push_back({a, b, kind});
+      } else {
+        p->pool.push_back(a);
+      }
+    }
+  }
 };
 
 static thread_local std::string g_err;
@@ -235,10 +280,13 @@ extern "C" int tr_plan_create(tr_plan** out, int device, int model, int n_featur
 
 extern "C" int tr_plan_destroy(tr_plan* p) {
   if (p == nullptr) return 0;
-  if (p->ws) {
-    (void)hipSetDevice(p->device);
-    (void)hipFree(p->ws);
+  (void)hipSetDevice(p->device);
+  for (auto& r : p->recs) {
+    (void)hipEventDestroy(r.a);
+    (void)hipEventDestroy(r.b);
   }
+  for (auto e : p->pool) (void)hipEventDestroy(e);
+  if (p->ws) (void)hipFree(p->ws);
   delete p;
   return 0;
 }
@@ -253,6 +301,7 @@ extern "C" int64_t tr_plan_workspace_bytes(const tr_plan* p) { return p ? (int64
 extern "C" const char* tr_plan_describe(const tr_plan* p) { return p ? p->desc.c_str() : ""; }
 
 static int factor_prep(tr_plan* p, const float* params, const float* w, const int32_t* stop, hipStream_t st) {
+  TimedLaunch tl(p, st, TR_KERNEL_PREP);
   TR_HIP(launch_prep_factors(p->fs, params, p->sp_beta, p->sp_thr, p->phi, p->dphi, stop, st));
   TR_HIP(launch_build_dense(p->fs, p->phi, w, p->dense, stop, st));
   return 0;
@@ -278,8 +327,8 @@ extern "C" int tr_loss_grad(tr_plan* p, const float* X, int64_t n_rows, const vo
                             const float* class_weight, double norm, const float* params, const float* weights,
                             float* grad_out, float* yhat_out, const int32_t* stop_flag, void* stream) {
   if (p == nullptr) return fail(TR_E_ARG, "plan is NULL");
-  if (X == nullptr || target == nullptr || params == nullptr || weights == nullptr || grad_out == nullptr)
-    return fail(TR_E_ARG, "NULL buffer");
+  if (params == nullptr || weights == nullptr || grad_out == nullptr) return fail(TR_E_ARG, "NULL buffer");
+  if (n_rows > 0 && (X == nullptr || target == nullptr)) return fail(TR_E_ARG, "NULL X / target");
   if (p->model == TR_MODEL_MULTINOMIAL && class_weight == nullptr)
     return fail(TR_E_ARG, "multinomial model needs class_weight");
   if (n_rows < 0 || n_rows > p->max_rows) return fail(TR_E_ARG, "n_rows exceeds the plan's max_rows");
@@ -305,12 +354,19 @@ extern "C" int tr_loss_grad(tr_plan* p, const float* X, int64_t n_rows, const vo
       TR_HIP(launch_rows(1, MODE_LIN_PRED, p->W, X, N, p->P, p->dense, bias, nullptr, nullptr, 0.f, yhat_out,
                          nullptr, nullptr, stop_flag, st));
     const int64_t rpw = (N + p->fgrid - 1) / p->fgrid;
-    TR_HIP(launch_linear_fused(p->fT, p->fCH, p->fgrid, X, N, p->P, p->dense, bias, (const float*)target,
-                               (float)(2.0 / norm), p->gpart, p->dpart, yhat_out, rpw, reverse, stop_flag, st));
-    TR_HIP(launch_reduce_slabs(4, p->gpart, p->fgrid, p->P, p->G, p->dpart, p->fgrid, 1.0 / norm, loss_slot,
-                               bias_slot, stop_flag, st));
+    {
+      TimedLaunch tl(p, st, TR_KERNEL_STREAM_FUSED);
+      TR_HIP(launch_linear_fused(p->fT, p->fCH, p->fgrid, X, N, p->P, p->dense, bias, (const float*)target,
+                                 (float)(2.0 / norm), p->gpart, p->dpart, yhat_out, rpw, reverse, stop_flag, st));
+    }
+    {
+      TimedLaunch tl(p, st, TR_KERNEL_REDUCE);
+      TR_HIP(launch_reduce_slabs(4, p->gpart, p->fgrid, p->P, p->G, p->dpart, p->fgrid, 1.0 / norm, loss_slot,
+                                 bias_slot, stop_flag, st));
+    }
   } else {
     const int C = p->C;
+    TimedLaunch* tl_rows = new TimedLaunch(p, st, TR_KERNEL_STREAM_ROWS);
     if (p->model == TR_MODEL_LINEAR) {
       TR_HIP(launch_rows(1, MODE_LIN_TRAIN, p->W, X, N, p->P, p->dense, bias, target, nullptr,
                          (float)(2.0 / norm), p->rowbuf, p->dpart, yhat_out, stop_flag, st));
@@ -318,6 +374,7 @@ extern "C" int tr_loss_grad(tr_plan* p, const float* X, int64_t n_rows, const vo
       TR_HIP(launch_rows(C, MODE_MNL_TRAIN, p->W, X, N, p->P, p->dense, nullptr, target, class_weight,
                          (float)(1.0 / norm), p->rowbuf, p->dpart, nullptr, stop_flag, st));
     }
+    delete tl_rows;
     const int64_t nd = rows_num_waves(C, N);
     const int cw = cols_cw(C);
     const int64_t PW = p->P / p->W;
@@ -329,11 +386,20 @@ extern "C" int tr_loss_grad(tr_plan* p, const float* X, int64_t n_rows, const vo
     if (nchunks < 1) nchunks = 1;
     const int64_t rpc = (N + nchunks - 1) / nchunks;
     nchunks = (N + rpc - 1) / rpc;
-    TR_HIP(launch_cols(C, p->W, nstripes, nchunks, X, N, p->P, p->rowbuf, rpc, p->gpart, 1, stop_flag, st));
-    TR_HIP(launch_reduce_slabs(p->W, p->gpart, nchunks, p->ncols, p->G, p->dpart, nd, 1.0 / norm, loss_slot,
-                               bias_slot, stop_flag, st));
+    {
+      TimedLaunch tl(p, st, TR_KERNEL_STREAM_COLS);
+      TR_HIP(launch_cols(C, p->W, nstripes, nchunks, X, N, p->P, p->rowbuf, rpc, p->gpart, 1, stop_flag, st));
+    }
+    {
+      TimedLaunch tl(p, st, TR_KERNEL_REDUCE);
+      TR_HIP(launch_reduce_slabs(p->W, p->gpart, nchunks, p->ncols, p->G, p->dpart, nd, 1.0 / norm, loss_slot,
+                                 bias_slot, stop_flag, st));
+    }
   }
-  TR_HIP(launch_mttkrp(p->fs, p->phi, p->dphi, weights, p->G, grad_out, stop_flag, st));
+  {
+    TimedLaunch tl(p, st, TR_KERNEL_MTTKRP);
+    TR_HIP(launch_mttkrp(p->fs, p->phi, p->dphi, weights, p->G, grad_out, stop_flag, st));
+  }
   return 0;
 }
 
@@ -386,7 +452,36 @@ extern "C" int tr_adam_step(tr_plan* p, float* params, const float* grad, float*
   ua.iter = iter;
   ua.patience = patience;
   ua.tol = tol;
+  TimedLaunch tl(p, (hipStream_t)stream, TR_KERNEL_UPDATE);
   TR_HIP(launch_update(p->fs, p->has_bias, params, grad, ua, exp_avg, exp_avg_sq, max_exp_avg_sq, nullptr, nullptr,
                        loss_hist, stop_flag, (hipStream_t)stream));
+  return 0;
+}
+
+extern "C" int tr_plan_set_timing(tr_plan* p, int enable) {
+  if (p == nullptr) return fail(TR_E_ARG, "plan is NULL");
+  p->timing = enable ? 1 : 0;
+  return 0;
+}
+
+extern "C" int tr_plan_read_timing(tr_plan* p, double* total_ms, int64_t* launches) {
+  if (p == nullptr || total_ms == nullptr || launches == nullptr) return fail(TR_E_ARG, "NULL argument");
+  for (int k = 0; k < TR_KERNEL_NKINDS; ++k) {
+    total_ms[k] = 0.0;
+    launches[k] = 0;
+  }
+  TR_HIP(hipSetDevice(p->device));
+  for (auto& r : p->recs) {
+    TR_HIP(hipEventSynchronize(r.b));
+    float ms = 0.f;
+    TR_HIP(hipEventElapsedTime(&ms, r.a, r.b));
+    if (r.kind >= 0 && r.kind < TR_KERNEL_NKINDS) {
+      total_ms[r.kind] += ms;
+      launches[r.kind] += 1;
+    }
+    p->pool.push_back(r.a);
+    p->pool.push_back(r.b);
+  }
+  p->recs.clear();
   return 0;
 }

@@ -35,6 +35,8 @@ def load(name):
         d["Bcp_final_list"] = split(d["Bcp_final"], shapes)
     if "grads0" in d:
         d["grads0_list"] = split(d["grads0"], shapes)
+    if "Bcp_10" in d:
+        d["Bcp_10_list"] = split(d["Bcp_10"], shapes)
     if "Bcp_final2" in d:
         d["Bcp_final2_list"] = split(d["Bcp_final2"], shapes)
     d["meta"] = meta

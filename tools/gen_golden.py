@@ -63,10 +63,19 @@ def linear_case(name, seed, shape, rank, non_negative, bias_init, lam, adam_kwar
     for A in m.Bcp:
         A.grad = None
     m.bias.grad = None
+    # 10-iteration snapshot from the same initial point (a fresh model, same seed)
+    torch.manual_seed(seed)
+    m10 = STR.CP_linear_regression(X.shape, rank=rank, non_negative=non_negative, bias_init=bias_init,
+                                   softplus_kwargs=softplus)
+    m10.fit_Adam(X, y, lambda_L2=lam, max_iter=min(10, iters), tol=tol, patience=patience, verbose=False,
+                 Adam_kwargs=dict(adam_kwargs))
     conv = m.fit_Adam(X, y, lambda_L2=lam, max_iter=iters, tol=tol, patience=patience, verbose=False,
                       Adam_kwargs=dict(adam_kwargs))
-    out = dict(X_q=Xq, y=y.numpy(), Bcp0=np.array(Bcp0, dtype=object) if False else np.concatenate(
-        [a.reshape(-1) for a in Bcp0]), bias0=b0, y_hat0=y_hat.detach().numpy(), loss0=np.float64(loss.item()),
+    out = dict(
+        Bcp_10=np.concatenate([A.detach().numpy().reshape(-1) for A in m10.Bcp]),
+        bias_10=m10.bias.detach().numpy().copy(), loss_running_10=np.array(m10.loss_running),
+        X_q=Xq, y=y.numpy(), Bcp0=np.concatenate([a.reshape(-1) for a in Bcp0]), bias0=b0,
+        y_hat0=y_hat.detach().numpy(), loss0=np.float64(loss.item()),
         grads0=np.concatenate([g.reshape(-1) for g in grads]), bias_grad0=bgrad,
         loss_running=np.array(m.loss_running, dtype=np.float64),
         Bcp_final=np.concatenate([A.detach().numpy().reshape(-1) for A in m.Bcp]),
@@ -119,6 +128,10 @@ def mnl_case(name, seed, shape, n_classes, rank, non_negative, class_w, lam, ada
     grads = [A.grad.numpy().copy() for A in m.Bcp]
     for A in m.Bcp:
         A.grad = None
+    torch.manual_seed(seed)
+    m10 = MTR.CP_logistic_regression(X.numpy(), y, rank=rank, non_negative=non_negative)
+    m10.fit_Adam(lambda_L2=lam, max_iter=min(10, iters), tol=tol, patience=patience, weights=np.asarray(class_w),
+                 verbose=False, Adam_kwargs=dict(adam_kwargs))
     conv = m.fit_Adam(lambda_L2=lam, max_iter=iters, tol=tol, patience=patience, weights=np.asarray(class_w),
                       verbose=False, Adam_kwargs=dict(adam_kwargs))
     meta = dict(model="multinomial", seed=seed, shape=list(shape), n_classes=n_classes, rank=rank,
@@ -131,7 +144,8 @@ def mnl_case(name, seed, shape, n_classes, rank, non_negative, class_w, lam, ada
          grads0=np.concatenate([g.reshape(-1) for g in grads]),
          loss_running=np.array(m.loss_running, dtype=np.float64),
          Bcp_final=np.concatenate([A.detach().numpy().reshape(-1) for A in m.Bcp]), converged=np.int32(conv),
-         meta=np.array(json.dumps(meta)))
+         Bcp_10=np.concatenate([A.detach().numpy().reshape(-1) for A in m10.Bcp]),
+         loss_running_10=np.array(m10.loss_running), meta=np.array(json.dumps(meta)))
 
 
 def init_case(name):
