@@ -210,6 +210,17 @@ extern "C" int tr_plan_create(tr_plan** out, int device, int model, int n_featur
     ds *= fs.dim[f];
   }
   if (model == TR_MODEL_MULTINOMIAL) fs.stride[n_feature_modes] = P;
+  for (int f = 0; f < nf; ++f) {  // other factors of f by decreasing dense stride (MTTKRP walk order)
+    int k = 0;
+    for (int g = 0; g < nf; ++g)
+      if (g != f) fs.others[f][k++] = (int8_t)g;
+    for (int a = 1; a < k; ++a)
+      for (int b = a; b > 0 && fs.stride[fs.others[f][b - 1]] < fs.stride[fs.others[f][b]]; --b) {
+        const int8_t t = fs.others[f][b];
+        fs.others[f][b] = fs.others[f][b - 1];
+        fs.others[f][b - 1] = t;
+      }
+  }
   p->nparams = fs.nfelem + (p->has_bias ? 1 : 0);
   p->ngrads = p->nparams + 1;
   p->W = (P % 4 == 0) ? 4 : 1;
@@ -302,8 +313,7 @@ extern "C" const char* tr_plan_describe(const tr_plan* p) { return p ? p->desc.c
 
 static int factor_prep(tr_plan* p, const float* params, const float* w, const int32_t* stop, hipStream_t st) {
   TimedLaunch tl(p, st, TR_KERNEL_PREP);
-  TR_HIP(launch_prep_factors(p->fs, params, p->sp_beta, p->sp_thr, p->phi, p->dphi, stop, st));
-  TR_HIP(launch_build_dense(p->fs, p->phi, w, p->dense, stop, st));
+  TR_HIP(launch_build_dense(p->fs, params, p->sp_beta, p->sp_thr, p->phi, p->dphi, w, p->dense, stop, st));
   return 0;
 }
 

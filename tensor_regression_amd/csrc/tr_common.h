@@ -27,6 +27,7 @@ struct FactorSet {
   int nonneg[TR_MAXF];       // softplus applied to this factor
   int64_t total;             // prod_f I_f
   int64_t nfelem;            // sum_f I_f * R
+  int8_t others[TR_MAXF][TR_MAXF];  // for each f: the other factors, by decreasing dense stride
 };
 
 // torch.nn.functional.softplus(x, beta, threshold) and its derivative

@@ -33,8 +33,9 @@ struct UpdateArgs {
 // Launch helpers (all asynchronous on `st`).  Return hipError_t of the launch.
 hipError_t launch_prep_factors(const FactorSet& fs, const float* params, float beta, float thr,
                                float* phi, float* dphi, const int32_t* stop, hipStream_t st);
-hipError_t launch_build_dense(const FactorSet& fs, const float* phi, const float* w, float* dense,
-                              const int32_t* stop, hipStream_t st);
+// softplus + dense B (one launch when the factors fit LDS, else prep + build)
+hipError_t launch_build_dense(const FactorSet& fs, const float* params, float beta, float thr, float* phi,
+                              float* dphi, const float* w, float* dense, const int32_t* stop, hipStream_t st);
 bool linear_fused_supported(int T, int CH);
 hipError_t launch_linear_fused(int T, int CH, int grid, const float* X, int64_t N, int64_t P,
                                const float* B, const float* bias, const float* y, float scale,

@@ -56,17 +56,41 @@ __global__ __launch_bounds__(256) void k_prep_factors(FactorSet fs, const float*
 
 // ==========================================================================================
 // K1b: dense coefficient tensor (tensorly cp_to_tensor, called at standard…py:124,
-// multinomial…py:182).  Factor columns are staged in LDS (sum_f I_f * R floats).
+// multinomial…py:182), fused with non_neg_fn: every workgroup stages the raw factors in LDS and
+// applies softplus there (sum_f I_f * R floats); workgroup 0 also publishes Phi and softplus'
+// for the gradient kernels.  Factor sets too large for LDS fall back to k_prep_factors + global.
 // ==========================================================================================
-__global__ __launch_bounds__(256) void k_build_dense(FactorSet fs, const float* __restrict__ phi,
-                                                     const float* __restrict__ w,
+__device__ __forceinline__ int tr_factor_of(const FactorSet& fs, int64_t e) {
+  int f = 0;
+#pragma unroll
+  for (int g = 1; g < TR_MAXF; ++g)
+    if (g < fs.nf && e >= fs.off[g]) f = g;
+  return f;
+}
+
+__global__ __launch_bounds__(256) void k_build_dense(FactorSet fs, const float* __restrict__ params,
+                                                     float beta, float thr, float* __restrict__ phi,
+                                                     float* __restrict__ dphi, const float* __restrict__ w,
                                                      float* __restrict__ dense, int use_lds,
                                                      const int32_t* __restrict__ stop) {
   extern __shared__ __attribute__((aligned(16))) float sphi[];
   if (stop != nullptr && *stop != 0) return;
   const float* F = phi;
   if (use_lds) {
-    for (int64_t k = threadIdx.x; k < fs.nfelem; k += blockDim.x) sphi[k] = phi[k];
+    const bool publish = blockIdx.x == 0;
+    for (int64_t k = threadIdx.x; k < fs.nfelem; k += blockDim.x) {
+      const float a = params[k];
+      float v = a, d = 1.0f;
+      if (fs.nonneg[tr_factor_of(fs, k)]) {
+        v = tr_softplus(a, beta, thr);
+        d = tr_softplus_grad(a, beta, thr);
+      }
+      sphi[k] = v;
+      if (publish) {
+        phi[k] = v;
+        dphi[k] = d;
+      }
+    }
     __syncthreads();
     F = sphi;
   }
@@ -473,21 +497,23 @@ __global__ __launch_bounds__(256) void k_cols(const float* __restrict__ X, int64
 
 // ==========================================================================================
 // K4: fixed-order slab reduction  out[col] = sum_k part[k][col]  (+ scalar partials)
-// Workgroup = 4 waves x 64 vector columns; wave q sums slabs q, q+4, ...; the 4 wave sums
-// are combined in order through LDS.  Block 0 also reduces the per-wave/per-WG fp64 scalar
-// partials (loss, bias gradient) and writes them into the gradient arena.
+// Workgroup = 16 waves x 64 vector columns; wave q sums slabs q, q+16, q+32, ... (4 loads in
+// flight per lane); the 16 wave sums are combined in wave order through LDS (deterministic).
+// Block 0 also reduces the per-wave/per-WG fp64 scalar partials (loss, bias gradient) and
+// writes them into the gradient arena.
 // ==========================================================================================
 template <int W>
-__global__ __launch_bounds__(256) void k_reduce_slabs(const float* __restrict__ part, int64_t nslabs,
-                                                      int64_t ncols, float* __restrict__ out,
-                                                      const double* __restrict__ dpart, int64_t nd,
-                                                      double loss_scale, float* __restrict__ loss_slot,
-                                                      float* __restrict__ bias_slot,
-                                                      const int32_t* __restrict__ stop) {
+__global__ __launch_bounds__(1024) void k_reduce_slabs(const float* __restrict__ part, int64_t nslabs,
+                                                       int64_t ncols, float* __restrict__ out,
+                                                       const double* __restrict__ dpart, int64_t nd,
+                                                       double loss_scale, float* __restrict__ loss_slot,
+                                                       float* __restrict__ bias_slot,
+                                                       const int32_t* __restrict__ stop) {
   using V = VecT<W>;
   using VT = typename V::T;
-  __shared__ VT sred[4][TR_WAVE];
-  __shared__ double dred[2][4];
+  constexpr int NWV = 16;
+  __shared__ VT sred[NWV][TR_WAVE];
+  __shared__ double dred[2][NWV];
   if (stop != nullptr && *stop != 0) return;
   const int lane = threadIdx.x & (TR_WAVE - 1);
   const int q = threadIdx.x / TR_WAVE;
@@ -495,23 +521,26 @@ __global__ __launch_bounds__(256) void k_reduce_slabs(const float* __restrict__ 
   const int64_t colv = (int64_t)blockIdx.x * TR_WAVE + lane;
   const VT* pv = reinterpret_cast<const VT*>(part);
   if (colv < NCW) {
-    VT a0 = V::zero(), a1 = V::zero();
+    VT a0 = V::zero(), a1 = V::zero(), a2 = V::zero(), a3 = V::zero();
     int64_t k = q;
-    for (; k + 4 < nslabs; k += 8) {
+    for (; k + 3 * NWV < nslabs; k += 4 * NWV) {
       const VT u0 = pv[k * NCW + colv];
-      const VT u1 = pv[(k + 4) * NCW + colv];
+      const VT u1 = pv[(k + NWV) * NCW + colv];
+      const VT u2 = pv[(k + 2 * NWV) * NCW + colv];
+      const VT u3 = pv[(k + 3 * NWV) * NCW + colv];
       a0 = V::add(a0, u0);
       a1 = V::add(a1, u1);
+      a2 = V::add(a2, u2);
+      a3 = V::add(a3, u3);
     }
-    if (k < nslabs) a0 = V::add(a0, pv[k * NCW + colv]);
-    sred[q][lane] = V::add(a0, a1);
+    for (; k < nslabs; k += NWV) a0 = V::add(a0, pv[k * NCW + colv]);
+    sred[q][lane] = V::add(V::add(a0, a1), V::add(a2, a3));
   }
   __syncthreads();
   if (q == 0 && colv < NCW) {
     VT s = sred[0][lane];
-    s = V::add(s, sred[1][lane]);
-    s = V::add(s, sred[2][lane]);
-    s = V::add(s, sred[3][lane]);
+#pragma unroll
+    for (int w = 1; w < NWV; ++w) s = V::add(s, sred[w][lane]);
     reinterpret_cast<VT*>(out)[colv] = s;
   }
   if (blockIdx.x == 0 && dpart != nullptr) {
@@ -528,8 +557,11 @@ __global__ __launch_bounds__(256) void k_reduce_slabs(const float* __restrict__ 
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-      const double l = ((dred[0][0] + dred[0][1]) + dred[0][2]) + dred[0][3];
-      const double b = ((dred[1][0] + dred[1][1]) + dred[1][2]) + dred[1][3];
+      double l = 0.0, b = 0.0;
+      for (int w = 0; w < NWV; ++w) {
+        l += dred[0][w];
+        b += dred[1][w];
+      }
       *loss_slot = (float)(l * loss_scale);
       if (bias_slot != nullptr) *bias_slot = (float)b;
     }
@@ -539,55 +571,110 @@ __global__ __launch_bounds__(256) void k_reduce_slabs(const float* __restrict__ 
 // ==========================================================================================
 // K5: MTTKRP + softplus chain: grad[A_f][i, r] = dphi * w_r * sum_{e: i_f(e)=i} G[e] prod_{g!=f} Phi_g[i_g(e), r]
 // (the autograd of cp_to_tensor + non_neg_fn, standard…py:462).  One workgroup per factor row.
+// The NO "other" modes are walked with a division-free mixed-radix counter whose fastest digit
+// is the mode with the smallest dense stride (most contiguous G reads); U gathers of G are
+// issued before they are consumed (G is L2-resident, so the loop is latency-, not
+// bandwidth-bound); factor columns sit in LDS; fixed-order block reduction over rank columns.
 // ==========================================================================================
-template <int RMAX>
+template <int RMAX, int NO>
 __global__ __launch_bounds__(256) void k_mttkrp(FactorSet fs, const float* __restrict__ phi,
                                                 const float* __restrict__ dphi,
                                                 const float* __restrict__ w,
-                                                const float* __restrict__ G, float* __restrict__ grad,
+                                                const float* __restrict__ G, float* __restrict__ out,
                                                 int use_lds, const int32_t* __restrict__ stop) {
+  constexpr int U = RMAX >= 64 ? 4 : 8;
+  constexpr int NOD = NO > 0 ? NO : 1;
   extern __shared__ __attribute__((aligned(16))) float sphi[];
   __shared__ float red[4][RMAX];
+  __shared__ float sw[RMAX];
   if (stop != nullptr && *stop != 0) return;
   const int R = fs.rank;
-  // locate (f, i) for this block
-  int64_t b = blockIdx.x;
+  const int nf = fs.nf;
+  int b = blockIdx.x;
   int f = 0;
-  while (f < fs.nf - 1 && b >= fs.dim[f]) {
-    b -= fs.dim[f];
+  while (f < nf - 1 && b >= (int)fs.dim[f]) {
+    b -= (int)fs.dim[f];
     ++f;
   }
-  const int64_t i = b;
+  const int i = b;
   const float* F = phi;
   if (use_lds) {
-    for (int64_t k = threadIdx.x; k < fs.nfelem; k += blockDim.x) sphi[k] = phi[k];
-    __syncthreads();
+    for (int k = threadIdx.x; k < (int)fs.nfelem; k += blockDim.x) sphi[k] = phi[k];
     F = sphi;
   }
+  if (threadIdx.x < RMAX) sw[threadIdx.x] = threadIdx.x < R ? w[threadIdx.x] : 0.f;
+  __syncthreads();
+
+  // other modes ordered by decreasing dense stride (digit NO-1 = most contiguous), host-sorted
+  int od[NOD], ostr[NOD], ooff[NOD];
+#pragma unroll
+  for (int k = 0; k < NOD; ++k) {
+    if (k < NO) {
+      const int g = fs.others[f][k];
+      od[k] = (int)fs.dim[g];
+      ostr[k] = (int)fs.stride[g];
+      ooff[k] = (int)fs.off[g];
+    } else {
+      od[k] = 1;
+      ostr[k] = 0;
+      ooff[k] = 0;
+    }
+  }
+  const int nother = (int)(fs.total / fs.dim[f]);
+  const int base = i * (int)fs.stride[f];
+  // per-thread digit state of j = threadIdx.x, and the stride 256 in the same radix
+  int idx[NOD], sd[NOD];
+  {
+    int rem = threadIdx.x, rs = blockDim.x;
+#pragma unroll
+    for (int k = NOD - 1; k >= 0; --k) {
+      idx[k] = rem % od[k];
+      rem /= od[k];
+      sd[k] = rs % od[k];
+      rs /= od[k];
+    }
+  }
+  auto advance = [&]() {
+    int carry = 0;
+#pragma unroll
+    for (int k = NOD - 1; k >= 0; --k) {
+      int d = idx[k] + sd[k] + carry;
+      carry = 0;
+      while (d >= od[k]) {
+        d -= od[k];
+        ++carry;
+      }
+      idx[k] = d;
+    }
+  };
   float acc[RMAX];
 #pragma unroll
   for (int r = 0; r < RMAX; ++r) acc[r] = 0.f;
-  const int64_t nother = fs.total / fs.dim[f];
-  for (int64_t j = threadIdx.x; j < nother; j += blockDim.x) {
-    int64_t rem = j;
-    int64_t pos = i * fs.stride[f];
-    int64_t idx[TR_MAXF];
+  for (int j0 = threadIdx.x; j0 < nother; j0 += U * (int)blockDim.x) {
+    float gv[U];
+    int frow[U][NOD];
 #pragma unroll
-    for (int g = TR_MAXF - 1; g >= 0; --g) {
-      if (g < fs.nf && g != f) {
-        idx[g] = rem % fs.dim[g];
-        rem /= fs.dim[g];
-        pos += idx[g] * fs.stride[g];
+    for (int u = 0; u < U; ++u) {
+      const bool ok = j0 + u * (int)blockDim.x < nother;
+      int pos = base;
+#pragma unroll
+      for (int k = 0; k < NOD; ++k) {
+        pos += idx[k] * ostr[k];
+        frow[u][k] = ooff[k] + idx[k] * R;
       }
+      gv[u] = ok ? G[pos] : 0.f;
+      advance();
     }
-    const float gv = G[pos];
 #pragma unroll
-    for (int r = 0; r < RMAX; ++r) {
-      if (r < R) {
-        float prod = w[r];
-        for (int g = 0; g < fs.nf; ++g)
-          if (g != f) prod *= F[fs.off[g] + idx[g] * R + r];
-        acc[r] = fmaf(gv, prod, acc[r]);
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int r = 0; r < RMAX; ++r) {
+        if (r < R) {
+          float prod = sw[r];
+#pragma unroll
+          for (int k = 0; k < NO; ++k) prod *= F[frow[u][k] + r];
+          acc[r] = fmaf(gv[u], prod, acc[r]);
+        }
       }
     }
   }
@@ -603,9 +690,9 @@ __global__ __launch_bounds__(256) void k_mttkrp(FactorSet fs, const float* __res
   __syncthreads();
   if (threadIdx.x < R) {
     const int r = threadIdx.x;
-    const float s = ((red[0][r] + red[1][r]) + red[2][r]) + red[3][r];
-    const int64_t e = fs.off[f] + i * R + r;
-    grad[e] = s * dphi[e];
+    const float s2 = ((red[0][r] + red[1][r]) + red[2][r]) + red[3][r];
+    const int64_t e = fs.off[f] + (int64_t)i * R + r;
+    out[e] = s2 * dphi[e];
   }
 }
 
@@ -675,26 +762,37 @@ __global__ __launch_bounds__(1024) void k_update(FactorSet fs, int has_bias, flo
                                                  double* __restrict__ loss_hist,
                                                  int32_t* __restrict__ stop) {
 #pragma clang fp contract(off)
-  __shared__ float wsum[16];
+  __shared__ float wsum[TR_MAXF * 16];
   __shared__ float norms[TR_MAXF];
   if (stop != nullptr && *stop != 0) return;
   const int t = threadIdx.x;
   const int lane = t & (TR_WAVE - 1);
   const int q = t / TR_WAVE;
   const int NWV = blockDim.x / TR_WAVE;
-  // ||A_f||_F for every factor (raw parameters), fixed-order block reduction
-  for (int f = 0; f < fs.nf; ++f) {
-    const int64_t n = fs.dim[f] * fs.rank;
-    const float* a = params + fs.off[f];
-    float s = 0.f;
-    for (int64_t k = t; k < n; k += blockDim.x) s = fmaf(a[k], a[k], s);
-    s = tr_wave_allreduce(s);
-    if (lane == 0) wsum[q] = s;
+  // ||A_f||_F of every factor (raw parameters) in one pass; fixed-order block reduction
+  {
+    float accn[TR_MAXF];
+#pragma unroll
+    for (int f = 0; f < TR_MAXF; ++f) accn[f] = 0.f;
+    for (int64_t k = t; k < fs.nfelem; k += blockDim.x) {
+      const float a = params[k];
+      const int f = tr_factor_of(fs, k);
+#pragma unroll
+      for (int g = 0; g < TR_MAXF; ++g)
+        if (g == f) accn[g] = fmaf(a, a, accn[g]);
+    }
+#pragma unroll
+    for (int f = 0; f < TR_MAXF; ++f) {
+      if (f < fs.nf) {
+        const float v = tr_wave_allreduce(accn[f]);
+        if (lane == 0) wsum[f * 16 + q] = v;
+      }
+    }
     __syncthreads();
-    if (t == 0) {
+    if (t < fs.nf) {
       float tot = 0.f;
-      for (int k = 0; k < NWV; ++k) tot += wsum[k];
-      norms[f] = sqrtf(tot);
+      for (int k = 0; k < NWV; ++k) tot += wsum[t * 16 + k];
+      norms[t] = sqrtf(tot);
     }
     __syncthreads();
   }
@@ -705,9 +803,7 @@ __global__ __launch_bounds__(1024) void k_update(FactorSet fs, int has_bias, flo
     float g = grad[e];
     float p = params[e];
     if (e < nfe) {
-      int f = 0;
-      for (int k = 1; k < fs.nf; ++k)
-        if (e >= fs.off[k]) f = k;
+      const int f = tr_factor_of(fs, e);
       const float tt = lam / (2.0f * norms[f]);
       g = g + tt * (2.0f * p);
     }
@@ -771,14 +867,18 @@ hipError_t launch_prep_factors(const FactorSet& fs, const float* params, float b
 
 static const int64_t kLdsFactorLimit = 12288;  // floats of factor columns staged in LDS (48 KiB)
 
-hipError_t launch_build_dense(const FactorSet& fs, const float* phi, const float* w, float* dense,
-                              const int32_t* stop, hipStream_t st) {
+hipError_t launch_build_dense(const FactorSet& fs, const float* params, float beta, float thr, float* phi,
+                              float* dphi, const float* w, float* dense, const int32_t* stop, hipStream_t st) {
   const int use_lds = fs.nfelem <= kLdsFactorLimit;
+  if (!use_lds) {
+    hipError_t e = launch_prep_factors(fs, params, beta, thr, phi, dphi, stop, st);
+    if (e != hipSuccess) return e;
+  }
   int64_t blocks = cdiv(fs.total, 256);
   if (blocks > 1024) blocks = 1024;
   const size_t lds = use_lds ? (size_t)fs.nfelem * sizeof(float) : 0;
-  hipLaunchKernelGGL(k_build_dense, dim3((unsigned)blocks), dim3(256), lds, st, fs, phi, w, dense,
-                     use_lds, stop);
+  hipLaunchKernelGGL(k_build_dense, dim3((unsigned)blocks), dim3(256), lds, st, fs, params, beta, thr, phi, dphi,
+                     w, dense, use_lds, stop);
   return hipGetLastError();
 }
 
@@ -930,31 +1030,47 @@ hipError_t launch_reduce_slabs(int W, const float* part, int64_t nslabs, int64_t
                                float* bias_slot, const int32_t* stop, hipStream_t st) {
   const unsigned grid = cdiv(ncols / W, TR_WAVE);
   if (W == 4)
-    hipLaunchKernelGGL(k_reduce_slabs<4>, dim3(grid), dim3(256), 0, st, part, nslabs, ncols, out, dpart, nd,
+    hipLaunchKernelGGL(k_reduce_slabs<4>, dim3(grid), dim3(1024), 0, st, part, nslabs, ncols, out, dpart, nd,
                        loss_scale, loss_slot, bias_slot, stop);
   else
-    hipLaunchKernelGGL(k_reduce_slabs<1>, dim3(grid), dim3(256), 0, st, part, nslabs, ncols, out, dpart, nd,
+    hipLaunchKernelGGL(k_reduce_slabs<1>, dim3(grid), dim3(1024), 0, st, part, nslabs, ncols, out, dpart, nd,
                        loss_scale, loss_slot, bias_slot, stop);
   return hipGetLastError();
 }
 
 // ---- MTTKRP -----------------------------------------------------------------------------------
+template <int RMAX>
+static hipError_t mttkrp_launch_r(const FactorSet& fs, const float* phi, const float* dphi, const float* w,
+                                  const float* G, float* grad, int use_lds, const int32_t* stop, hipStream_t st,
+                                  dim3 grid, size_t lds) {
+  const dim3 block(256);
+#define TR_MTT(NO) \
+  hipLaunchKernelGGL((k_mttkrp<RMAX, NO>), grid, block, lds, st, fs, phi, dphi, w, G, grad, use_lds, stop)
+  switch (fs.nf - 1) {
+    case 0: TR_MTT(0); break;
+    case 1: TR_MTT(1); break;
+    case 2: TR_MTT(2); break;
+    case 3: TR_MTT(3); break;
+    case 4: TR_MTT(4); break;
+    case 5: TR_MTT(5); break;
+    case 6: TR_MTT(6); break;
+    default: TR_MTT(7); break;
+  }
+#undef TR_MTT
+  return hipGetLastError();
+}
+
 hipError_t launch_mttkrp(const FactorSet& fs, const float* phi, const float* dphi, const float* w,
                          const float* G, float* grad, const int32_t* stop, hipStream_t st) {
   int64_t rows = 0;
   for (int f = 0; f < fs.nf; ++f) rows += fs.dim[f];
   const int use_lds = fs.nfelem <= kLdsFactorLimit;
   const size_t lds = use_lds ? (size_t)fs.nfelem * sizeof(float) : 0;
-  const dim3 grid((unsigned)rows), block(256);
-  if (fs.rank <= 8)
-    hipLaunchKernelGGL(k_mttkrp<8>, grid, block, lds, st, fs, phi, dphi, w, G, grad, use_lds, stop);
-  else if (fs.rank <= 16)
-    hipLaunchKernelGGL(k_mttkrp<16>, grid, block, lds, st, fs, phi, dphi, w, G, grad, use_lds, stop);
-  else if (fs.rank <= 32)
-    hipLaunchKernelGGL(k_mttkrp<32>, grid, block, lds, st, fs, phi, dphi, w, G, grad, use_lds, stop);
-  else
-    hipLaunchKernelGGL(k_mttkrp<64>, grid, block, lds, st, fs, phi, dphi, w, G, grad, use_lds, stop);
-  return hipGetLastError();
+  const dim3 grid((unsigned)rows);
+  if (fs.rank <= 8) return mttkrp_launch_r<8>(fs, phi, dphi, w, G, grad, use_lds, stop, st, grid, lds);
+  if (fs.rank <= 16) return mttkrp_launch_r<16>(fs, phi, dphi, w, G, grad, use_lds, stop, st, grid, lds);
+  if (fs.rank <= 32) return mttkrp_launch_r<32>(fs, phi, dphi, w, G, grad, use_lds, stop, st, grid, lds);
+  return mttkrp_launch_r<64>(fs, phi, dphi, w, G, grad, use_lds, stop, st, grid, lds);
 }
 
 hipError_t launch_update(const FactorSet& fs, int has_bias, float* params, const float* grad,
