@@ -1,0 +1,133 @@
+"""CPU-side checks: the C-ABI library loads and exports every symbol the header declares, its
+argument validation works without a GPU, and the host-side Python logic (Adam kwargs resolution,
+softplus kwargs, quirk-compatible errors, the numpy pairwise-sum order restated in k_converge)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "tensor_regression_hip.h")
+
+
+def header_symbols():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|const char\*)\s+(tr_\w+)\s*\(", txt, flags=re.M)))
+
+
+def test_library_exports_every_header_symbol():
+    from tensor_regression_amd import _lib
+    lib = _lib.load()
+    syms = header_symbols()
+    assert len(syms) >= 14
+    for s in syms:
+        assert hasattr(lib, s), s
+        assert s in _lib.SIGNATURES, f"{s} has no ctypes signature"
+    assert set(_lib.SIGNATURES) == set(syms)
+    assert lib.tr_abi_version() == _lib.TR_ABI_VERSION
+
+
+def test_argument_validation_without_gpu():
+    from tensor_regression_amd import _lib
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    dims = (ctypes.c_int64 * 2)(8, 4)
+    nn = (ctypes.c_int32 * 3)(0, 0, 0)
+    # invalid arguments are rejected before any device call
+    assert lib.tr_plan_create(ctypes.byref(h), 0, 0, 0, dims, 1, 2, 10, nn, 50.0, 1.0) == -1
+    assert b"factors" in lib.tr_last_error()
+    assert lib.tr_plan_create(ctypes.byref(h), 0, 0, 2, dims, 1, 0, 10, nn, 50.0, 1.0) == -1
+    assert lib.tr_plan_create(ctypes.byref(h), 0, 1, 2, dims, 17, 2, 10, nn, 50.0, 1.0) == -2
+    assert lib.tr_plan_create(ctypes.byref(h), 0, 7, 2, dims, 1, 2, 10, nn, 50.0, 1.0) == -1
+    assert lib.tr_loss_grad(None, None, 0, None, None, 1.0, None, None, None, None, None, None) == -1
+    assert lib.tr_adam_step(None, None, None, None, None, None, 0.0, 0.0, 0.9, 0.999, 1e-8, 0.0, 0, 1, None,
+                            0, 0, 0, 0.0, None, None) == -1
+    import torch
+    if not torch.cuda.is_available():
+        # a well-formed plan needs a device: the failure is reported, not hidden
+        rc = lib.tr_plan_create(ctypes.byref(h), 0, 0, 2, dims, 1, 2, 10, nn, 50.0, 1.0)
+        assert rc > 0 and lib.tr_last_error()
+
+
+def test_no_cpu_fallback_in_product():
+    """The product package never imports the oracle."""
+    pkg = os.path.join(ROOT, "tensor_regression_amd")
+    for dp, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith(".py"):
+                src = open(os.path.join(dp, f)).read()
+                assert "oracle" not in re.sub(r"#.*", "", src).replace('"""', ""), f
+
+
+def test_adam_kwargs_resolution():
+    from tensor_regression_amd._engine import adam_hparams
+    with pytest.raises(TypeError):
+        adam_hparams(None)  # reference quirk Q1
+    hp = adam_hparams({"lr": 0.01})
+    assert hp == dict(lr=0.01, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.0, amsgrad=False)
+    hp = adam_hparams({"lr": 0.02, "betas": (0.8, 0.99), "eps": 1e-6, "weight_decay": 0.1, "amsgrad": True})
+    assert hp["beta1"] == 0.8 and hp["amsgrad"] is True and hp["weight_decay"] == 0.1
+    with pytest.raises(TypeError):
+        adam_hparams({"lr": 0.1, "bogus": 1})
+    with pytest.raises(ValueError):
+        adam_hparams({"lr": -1})
+    with pytest.raises(NotImplementedError):
+        adam_hparams({"lr": 0.1, "maximize": True})
+
+
+def test_softplus_kwargs():
+    from tensor_regression_amd._engine import softplus_params
+    assert softplus_params(None) == (50.0, 1.0)
+    assert softplus_params({"beta": 5}) == (5.0, 20.0)
+
+
+def _pairwise(a):
+    """numpy's DOUBLE_pairwise_sum order, as restated in k_converge (np_pairwise_sum_absdiff)."""
+    n = len(a)
+    if n < 8:
+        res = -0.0
+        for x in a:
+            res += x
+        return res
+    if n <= 128:
+        r = list(a[:8])
+        i = 8
+        while i < n - (n % 8):
+            for j in range(8):
+                r[j] += a[i + j]
+            i += 8
+        res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]))
+        while i < n:
+            res += a[i]
+            i += 1
+        return res
+    n2 = n // 2
+    n2 -= n2 % 8
+    return _pairwise(a[:n2]) + _pairwise(a[n2:])
+
+
+@pytest.mark.parametrize("seed", range(5))
+def test_plateau_sum_order_matches_numpy(seed):
+    rng = np.random.default_rng(seed)
+    for n in list(range(1, 40)) + [127, 128, 129, 300, 1000, 4097]:
+        h = rng.standard_normal(n + 1) * 10 ** rng.uniform(-6, 2)
+        d = np.abs(np.diff(h))
+        assert _pairwise(list(d)) == np.sum(d)
+
+
+def test_model_constructors_cpu_only():
+    """Construction and init (RNG-identical to the reference) need no GPU."""
+    import torch
+    from tensor_regression_amd import CP_linear_regression, CP_logistic_regression
+    torch.manual_seed(0)
+    m = CP_linear_regression((10, 6, 4), rank=3, non_negative=True)
+    assert [tuple(a.shape) for a in m.Bcp] == [(6, 3), (4, 3)] and m.non_negative == [True] * 3
+    assert all(a.requires_grad for a in m.Bcp) and m.bias.requires_grad
+    X = np.random.default_rng(0).standard_normal((20, 5, 3)).astype(np.float32)
+    y = np.arange(20) % 4
+    mm = CP_logistic_regression(X, y, rank=2)
+    assert mm.n_classes == 4 and [tuple(a.shape) for a in mm.Bcp] == [(5, 2), (3, 2), (4, 2)]
+    with pytest.raises(TypeError):
+        m.fit_Adam(torch.zeros(10, 6, 4), torch.zeros(10))

@@ -1,0 +1,158 @@
+"""Multi-rank fit loop on CPU (gloo, world_size 2).
+
+`tensor_regression_amd._engine.run_adam_fit` is the production fit loop: per iteration it calls
+the plan's data-gradient entry point, all-reduces the packed gradient arena, then the plan's
+Adam step. Here the HIP plan is replaced by `OraclePlan`, a test double with the same interface
+that computes shard gradients with the oracle. The real loop then runs sample-sharded over gloo
+and is compared with the unsharded run. This covers the sharding, the global normalisation, the
+all-reduce placement, the device-side history and stop-flag bookkeeping, and the replica
+lock-step, all without a GPU.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import cp_oracle
+from tensor_regression_amd._engine import adam_hparams, run_adam_fit
+
+
+class OraclePlan:
+    """Same interface as _engine.Plan, computed on the CPU with the oracle (tests only)."""
+
+    def __init__(self, model, shapes, non_negative, has_bias):
+        self.model = model
+        self.shapes = shapes
+        self.non_negative = non_negative
+        self.has_bias = has_bias
+        self.offsets = np.cumsum([0] + [a * b for a, b in shapes]).tolist()
+        self.num_params = self.offsets[-1] + (1 if has_bias else 0)
+        self.num_grads = self.num_params + 1
+        self.device_str = "cpu"
+
+    def factors(self, arena):
+        return [arena[self.offsets[f]:self.offsets[f + 1]].view(s).clone() for f, s in enumerate(self.shapes)]
+
+    def loss_grad(self, X, target, class_weight, norm, arena, weights, grad, yhat=None, stop=None):
+        if stop is not None and int(stop.item()):
+            return
+        Bcp = [a.clone().requires_grad_(True) for a in self.factors(arena)]
+        if self.model == "linear":
+            b = arena[-1:].clone().requires_grad_(True)
+            yh = cp_oracle.lin_model(X, Bcp, weights, self.non_negative, b)
+            data = torch.sum((yh - target) ** 2) / norm
+            data.backward()
+            grad[:self.offsets[-1]] = torch.cat([a.grad.reshape(-1) for a in Bcp])
+            grad[self.offsets[-1]] = b.grad[0]
+        else:
+            S = cp_oracle.mnl_model(X, Bcp, weights, self.non_negative)
+            logq = torch.log_softmax(S, dim=1)
+            cw = class_weight[target]
+            data = torch.sum(-cw * logq[torch.arange(X.shape[0]), target]) / norm
+            data.backward()
+            grad[:self.offsets[-1]] = torch.cat([a.grad.reshape(-1) for a in Bcp])
+        grad[-1] = data.detach()
+
+    def adam_step(self, arena, grad, m, v, vmax, lam, hp, step, hist, base, it, patience, tol, stop):
+        if int(stop.item()):
+            return
+        nfe = self.offsets[-1]
+        norms = [torch.sqrt(torch.sum(arena[self.offsets[f]:self.offsets[f + 1]] ** 2))
+                 for f in range(len(self.shapes))]
+        g = grad[:self.num_params].clone()
+        for f, n in enumerate(norms):
+            sl = slice(self.offsets[f], self.offsets[f + 1])
+            g[sl] += (lam / (2 * n)) * (2 * arena[sl])
+        if hp["weight_decay"]:
+            g = g + hp["weight_decay"] * arena[:self.num_params]
+        m.lerp_(g, 1 - hp["beta1"])
+        v.mul_(hp["beta2"]).addcmul_(g, g, value=1 - hp["beta2"])
+        bc1 = 1 - hp["beta1"] ** step
+        bc2 = 1 - hp["beta2"] ** step
+        den_src = v
+        if hp["amsgrad"]:
+            torch.maximum(vmax, v, out=vmax)
+            den_src = vmax
+        denom = den_src.sqrt() / (bc2 ** 0.5) + hp["eps"]
+        arena[:self.num_params].addcdiv_(m, denom, value=-hp["lr"] / bc1)
+        total = float(grad[-1]) + lam * float(sum(norms))
+        hist[base + it] = total
+        if it > patience and tol > 0:
+            h = hist[it - patience: base + it + 1].numpy()
+            if np.sum(np.abs(np.diff(h))) < tol:
+                stop[0] = it + 1
+        _ = nfe
+
+
+def _problem(model):
+    g = torch.Generator().manual_seed(7)
+    N, dims, R = 96, (6, 5), 3
+    X = torch.randn(N, *dims, generator=g)
+    if model == "linear":
+        shapes = [(d, R) for d in dims]
+        y = torch.randn(N, generator=g)
+        cw = None
+        norm = float(N)
+    else:
+        C = 4
+        shapes = [(d, R) for d in dims] + [(C, R)]
+        y = torch.randint(0, C, (N,), generator=g)
+        cw = torch.rand(C, generator=g) + 0.5
+        norm = float(cw[y].double().sum())
+    arena0 = torch.randn(sum(a * b for a, b in shapes) + (1 if model == "linear" else 0), generator=g) * 0.3
+    return X, y, cw, norm, shapes, arena0
+
+
+def _fit(model, X, y, cw, norm, shapes, arena0, allreduce=None, iters=25, tol=0.0, patience=5):
+    plan = OraclePlan(model, shapes, [False] * len(shapes), model == "linear")
+    arena = arena0.clone()
+    loss_running = []
+    hp = adam_hparams({"lr": 0.02, "amsgrad": model != "linear"})
+    conv, n = run_adam_fit(plan, X, y, cw, norm, arena, torch.ones(shapes[0][1]), 0.01, iters, tol, patience, hp,
+                           loss_running, allreduce=allreduce, sync_every=7)
+    return arena, loss_running, conv
+
+
+def _worker(rank, world, port, model, tol, out_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    X, y, cw, norm, shapes, arena0 = _problem(model)
+    lo, hi = [(0, 40), (40, 96)][rank]  # uneven shards
+    arena, lr_, conv = _fit(model, X[lo:hi].contiguous(), y[lo:hi].contiguous(), cw, norm, shapes, arena0,
+                            allreduce=lambda g: dist.all_reduce(g), tol=tol)
+    torch.save({"arena": arena, "loss_running": lr_, "conv": conv}, f"{out_path}.{rank}")
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("model,tol", [("linear", 0.0), ("multinomial", 0.0), ("linear", 0.05)])
+def test_sharded_fit_matches_unsharded(tmp_path, model, tol):
+    torch.set_num_threads(1)
+    X, y, cw, norm, shapes, arena0 = _problem(model)
+    ref_arena, ref_loss, ref_conv = _fit(model, X, y, cw, norm, shapes, arena0, tol=tol)
+    out = str(tmp_path / "res")
+    mp.spawn(_worker, args=(2, _free_port(), model, tol, out), nprocs=2, join=True)
+    r0 = torch.load(out + ".0", weights_only=True)
+    r1 = torch.load(out + ".1", weights_only=True)
+    # replicas in lock-step: bitwise identical on both ranks
+    assert torch.equal(r0["arena"], r1["arena"])
+    assert r0["loss_running"] == r1["loss_running"]
+    # and equal to the unsharded fit up to fp32 reduction order
+    assert len(r0["loss_running"]) == len(ref_loss)
+    assert bool(r0["conv"]) == bool(ref_conv)
+    np.testing.assert_allclose(r0["loss_running"], ref_loss, rtol=2e-5)
+    rel = float(torch.linalg.norm(r0["arena"] - ref_arena) / torch.linalg.norm(ref_arena))
+    assert rel < 1e-4, rel

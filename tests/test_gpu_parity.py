@@ -359,3 +359,21 @@ def test_predict_api():
     np.testing.assert_allclose(prob.sum(1), 1.0, rtol=1e-5)
     cm, acc = mm.make_confusion_matrix()
     assert cm.shape == (3, 3) and 0.0 <= acc <= 1.0
+
+
+def test_kat2_notebook_trace_on_gpu():
+    """KAT-2: demo_MultinomialTensorRegression.ipynb's printed 36-iteration Adam-amsgrad trace
+    (fp32 on the author's CUDA GPU), reproduced through the HIP path on the notebook's own inputs
+    (X (2000, 500, 500), 5 classes, rank 4).  The reference replays it to 3.8e-7 (kat_replay.json)."""
+    from kat_data import KAT2_TRACE, kat_inputs
+    from tensor_regression_amd import CP_logistic_regression
+    from tensor_regression_amd import multinomial_tensor_regression as M
+    X, y = kat_inputs("kat2")
+    M.make_BcpInit(np.concatenate((X.shape[1:], [5])), 4, [False] * 3, scale=1)  # the notebook's extra draw
+    m = CP_logistic_regression(X, y, rank=4, non_negative=[False] * 3, Bcp_init_scale=1, device=DEV,
+                               softplus_kwargs={'beta': 50, 'threshold': 1})
+    m.fit_Adam(lambda_L2=0.01, max_iter=len(KAT2_TRACE), tol=1e-6, patience=100, weights=np.ones(5),
+               Adam_kwargs={'lr': 0.01, 'amsgrad': True})
+    got = np.array(m.loss_running)
+    assert len(got) == len(KAT2_TRACE)
+    np.testing.assert_allclose(got, KAT2_TRACE, rtol=1e-5)
