@@ -33,6 +33,7 @@ struct tr_plan {
   int W = 4;
   // single-pass linear strategy
   int fused = 0, fT = 0, fCH = 0, fgrid = 0;
+  int mfma_rows = 0;  // multinomial forward on the matrix cores
   // two-pass strategy
   int64_t max_slabs = 0;
   // workspace
@@ -235,6 +236,7 @@ extern "C" int tr_plan_create(tr_plan** out, int device, int model, int n_featur
     p->ncu = ncu;
 
   choose_fused(p);
+  p->mfma_rows = (model == TR_MODEL_MULTINOMIAL && rows_mfma_supported(C, P) && !env_flag("TR_NO_MFMA")) ? 1 : 0;
 
   // two-pass slab budget: max(16 MiB, 2 % of X bytes)
   {
@@ -248,12 +250,14 @@ extern "C" int tr_plan_create(tr_plan** out, int device, int model, int n_featur
   }
   p->gpart_slabs = p->max_slabs;
   if (p->fused && p->fgrid > p->gpart_slabs) p->gpart_slabs = p->fgrid;
-  p->dpart_n = rows_num_waves(C, max_rows) + 64;
+  p->dpart_n = rows_num_waves(C, max_rows) + rows_mfma_num_waves(max_rows) + 64;
   if (p->fused && p->fgrid > p->dpart_n) p->dpart_n = p->fgrid;
 
   // workspace carve (256-B aligned pieces)
   auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
-  const size_t b_phi = al(fs.nfelem * 4), b_dense = al(p->ncols * 4), b_gpart = al((size_t)p->gpart_slabs * p->ncols * 4),
+  // dense B / G: class-major; padded to 16 class rows for the MFMA forward (pad rows stay zero)
+  const int64_t dense_rows = p->mfma_rows && C < 16 ? 16 : C;
+  const size_t b_phi = al(fs.nfelem * 4), b_dense = al((size_t)dense_rows * P * 4), b_gpart = al((size_t)p->gpart_slabs * p->ncols * 4),
                b_row = al((size_t)max_rows * C * 4), b_dpart = al((size_t)p->dpart_n * 2 * 8);
   p->ws_bytes = 2 * b_phi + 2 * b_dense + b_gpart + b_row + b_dpart;
   e = hipMalloc(&p->ws, p->ws_bytes);
@@ -279,10 +283,11 @@ extern "C" int tr_plan_create(tr_plan** out, int device, int model, int n_featur
 
   char buf[512];
   std::snprintf(buf, sizeof(buf),
-                "model=%s K=%d C=%d R=%d P=%lld nparams=%lld ncu=%d path=%s T=%d CH=%d grid=%d W=%d "
+                "model=%s K=%d C=%d R=%d P=%lld nparams=%lld ncu=%d path=%s%s T=%d CH=%d grid=%d W=%d "
                 "max_slabs=%lld workspace=%.1fMiB",
                 model == TR_MODEL_LINEAR ? "linear" : "multinomial", p->K, C, rank, (long long)P,
-                (long long)p->nparams, p->ncu, p->fused ? "fused-1pass" : "2pass", p->fT, p->fCH, p->fgrid,
+                (long long)p->nparams, p->ncu, p->fused ? "fused-1pass" : "2pass", p->mfma_rows ? "+mfma-fwd" : "", p->fT,
+                p->fCH, p->fgrid,
                 p->W, (long long)p->max_slabs, p->ws_bytes / 1048576.0);
   p->desc = buf;
   *out = p;
@@ -328,6 +333,11 @@ extern "C" int tr_forward(tr_plan* p, const float* X, int64_t n_rows, const floa
   int rc = factor_prep(p, params, weights, nullptr, st);
   if (rc) return rc;
   const int mode = p->model == TR_MODEL_LINEAR ? MODE_LIN_PRED : MODE_MNL_PRED;
+  if (p->mfma_rows) {
+    TR_HIP(launch_rows_mfma(MODE_MNL_PRED, X, n_rows, p->P, p->dense, p->C, nullptr, nullptr, 0.f, out, nullptr,
+                            nullptr, st));
+    return 0;
+  }
   TR_HIP(launch_rows(p->C, mode, p->W, X, n_rows, p->P, p->dense, params + p->fs.nfelem, nullptr, nullptr, 0.f,
                      out, nullptr, nullptr, nullptr, st));
   return 0;
@@ -380,12 +390,15 @@ extern "C" int tr_loss_grad(tr_plan* p, const float* X, int64_t n_rows, const vo
     if (p->model == TR_MODEL_LINEAR) {
       TR_HIP(launch_rows(1, MODE_LIN_TRAIN, p->W, X, N, p->P, p->dense, bias, target, nullptr,
                          (float)(2.0 / norm), p->rowbuf, p->dpart, yhat_out, stop_flag, st));
+    } else if (p->mfma_rows) {
+      TR_HIP(launch_rows_mfma(MODE_MNL_TRAIN, X, N, p->P, p->dense, C, (const int64_t*)target, class_weight,
+                              (float)(1.0 / norm), p->rowbuf, p->dpart, stop_flag, st));
     } else {
       TR_HIP(launch_rows(C, MODE_MNL_TRAIN, p->W, X, N, p->P, p->dense, nullptr, target, class_weight,
                          (float)(1.0 / norm), p->rowbuf, p->dpart, nullptr, stop_flag, st));
     }
     delete tl_rows;
-    const int64_t nd = rows_num_waves(C, N);
+    const int64_t nd = p->mfma_rows ? rows_mfma_num_waves(N) : rows_num_waves(C, N);
     const int cw = cols_cw(C);
     const int64_t PW = p->P / p->W;
     const int64_t nstripes = (PW + 256 * cw - 1) / (256 * cw);

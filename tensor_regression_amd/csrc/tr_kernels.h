@@ -50,6 +50,11 @@ hipError_t launch_rows(int C, int mode, int W, const float* X, int64_t N, int64_
                        float scale, float* out, double* dpart, float* yhat, const int32_t* stop,
                        hipStream_t st);
 int64_t rows_num_waves(int C, int64_t N);
+bool rows_mfma_supported(int C, int64_t P);
+int64_t rows_mfma_num_waves(int64_t N);
+hipError_t launch_rows_mfma(int mode, const float* X, int64_t N, int64_t P, const float* Bt, int C,
+                            const int64_t* lab, const float* class_w, float scale, float* out, double* dpart,
+                            const int32_t* stop, hipStream_t st);
 hipError_t launch_cols(int C, int W, int64_t nstripes, int64_t nchunks, const float* X, int64_t N,
                        int64_t P, const float* V, int64_t rows_per_chunk, float* gpart, int reverse,
                        const int32_t* stop, hipStream_t st);

@@ -424,6 +424,148 @@ __global__ __launch_bounds__(256) void k_rows(
 }
 
 // ==========================================================================================
+// K2m: multinomial forward on the matrix cores.  Z (rows x C) = X (rows x P) . B (P x C) with
+// v_mfma_f32_16x16x4_f32 (exact fp32, C padded to 16 lanes), fused double-softmax CE / dZ
+// epilogue.  A wave owns RT tiles of 16 rows; per 32-deep k step each lane loads two float4 of
+// X (its row, 8 consecutive features: 4 lanes cover a full 128-B line) and two float4 of the
+// class-major Bt (shared by the RT row tiles), then issues 8*RT MFMAs.  Lane l supplies
+// A[i=l&15][k=l>>4] and B[k=l>>4][j=l&15]; MFMA m of a step uses feature k0 + 8*(l>>4) + m on
+// both operands, so the k order is permuted consistently.  Accumulator layout: class = l&15,
+// row = 4*(l>>4) + reg.  Class reductions are 16-lane swizzle butterflies (deterministic).
+// ==========================================================================================
+template <int PATTERN>
+__device__ __forceinline__ float tr_swz(float v) {
+  return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), PATTERN));
+}
+__device__ __forceinline__ float tr_sum16(float v) {
+  v += tr_swz<0x201F>(v);  // xor 8
+  v += tr_swz<0x101F>(v);  // xor 4
+  v += tr_swz<0x081F>(v);  // xor 2
+  v += tr_swz<0x041F>(v);  // xor 1
+  return v;
+}
+__device__ __forceinline__ float tr_max16(float v) {
+  v = fmaxf(v, tr_swz<0x201F>(v));
+  v = fmaxf(v, tr_swz<0x101F>(v));
+  v = fmaxf(v, tr_swz<0x081F>(v));
+  v = fmaxf(v, tr_swz<0x041F>(v));
+  return v;
+}
+
+typedef float tr_f32x4 __attribute__((ext_vector_type(4)));
+
+template <int MODE, int RT>
+__global__ __launch_bounds__(256) void k_rows_mfma(
+    const float* __restrict__ X, int64_t N, int64_t P, const float* __restrict__ Bt, int C,
+    const int64_t* __restrict__ lab, const float* __restrict__ class_w, float scale,
+    float* __restrict__ out, double* __restrict__ dpart, const int32_t* __restrict__ stop) {
+  if (stop != nullptr && *stop != 0) return;
+  const int lane = threadIdx.x & (TR_WAVE - 1);
+  const int64_t gw = (int64_t)blockIdx.x * (blockDim.x / TR_WAVE) + (threadIdx.x / TR_WAVE);
+  const int64_t row0 = gw * (16 * RT);
+  const int i = lane & 15;  // A row in tile / class column
+  const int g = lane >> 4;  // k group
+  if (row0 >= N) {
+    if (MODE == MODE_MNL_TRAIN && lane == 0) {
+      dpart[2 * gw] = 0.0;
+      dpart[2 * gw + 1] = 0.0;
+    }
+    return;
+  }
+  const float4* xr[RT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    int64_t r = row0 + rt * 16 + i;
+    r = r < N ? r : N - 1;
+    xr[rt] = reinterpret_cast<const float4*>(X + r * P + 8 * g);
+  }
+  const bool cls_ok = i < C;
+  // Bt is padded to 16 class rows (rows >= C are zero): unconditional loads, no per-lane branches
+  const float4* br = reinterpret_cast<const float4*>(Bt + (int64_t)i * P + 8 * g);
+  tr_f32x4 acc[RT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) acc[rt] = tr_f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nsteps = (int)(P / 32);
+  auto step = [&](const float4(&xa)[RT], const float4(&xb)[RT], const float4 ba, const float4 bb) {
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      acc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[rt].x, ba.x, acc[rt], 0, 0, 0);
+      acc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[rt].y, ba.y, acc[rt], 0, 0, 0);
+      acc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[rt].z, ba.z, acc[rt], 0, 0, 0);
+      acc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[rt].w, ba.w, acc[rt], 0, 0, 0);
+      acc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(xb[rt].x, bb.x, acc[rt], 0, 0, 0);
+      acc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(xb[rt].y, bb.y, acc[rt], 0, 0, 0);
+      acc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(xb[rt].z, bb.z, acc[rt], 0, 0, 0);
+      acc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(xb[rt].w, bb.w, acc[rt], 0, 0, 0);
+    }
+  };
+  int st = 0;
+  for (; st + 1 < nsteps; st += 2) {  // two k steps of loads in flight before the MFMAs
+    float4 xa0[RT], xb0[RT], xa1[RT], xb1[RT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      xa0[rt] = xr[rt][8 * st];
+      xb0[rt] = xr[rt][8 * st + 1];
+      xa1[rt] = xr[rt][8 * st + 8];
+      xb1[rt] = xr[rt][8 * st + 9];
+    }
+    const float4 ba0 = br[8 * st], bb0 = br[8 * st + 1];
+    const float4 ba1 = br[8 * st + 8], bb1 = br[8 * st + 9];
+    __builtin_amdgcn_sched_barrier(0);  // keep all 4*RT+4 loads of the two steps in flight together
+    step(xa0, xb0, ba0, bb0);
+    step(xa1, xb1, ba1, bb1);
+  }
+  if (st < nsteps) {
+    float4 xa0[RT], xb0[RT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      xa0[rt] = xr[rt][8 * st];
+      xb0[rt] = xr[rt][8 * st + 1];
+    }
+    const float4 ba0 = br[8 * st], bb0 = br[8 * st + 1];
+    step(xa0, xb0, ba0, bb0);
+  }
+  const float NEG = -__builtin_huge_valf();
+  double lsum = 0.0;
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const int64_t row = row0 + rt * 16 + 4 * g + reg;
+      const float z = cls_ok ? acc[rt][reg] : NEG;
+      const float mx = tr_max16(z);
+      const float ez = cls_ok ? expf(z - mx) : 0.f;
+      const float sum = tr_sum16(ez);
+      const float S = ez * (1.0f / sum);
+      if (MODE == MODE_MNL_PRED) {
+        if (cls_ok && row < N) out[row * C + i] = S;
+        continue;
+      }
+      // CrossEntropyLoss(weight) on the probabilities S (double softmax)
+      const float m2 = tr_max16(cls_ok ? S : NEG);
+      const float q = cls_ok ? expf(S - m2) : 0.f;
+      const float s2 = tr_sum16(q);
+      const float lse = logf(s2);
+      const bool valid = row < N;
+      const int64_t yl = valid ? lab[row] : -1;
+      const float cw = valid ? class_w[yl] : 0.f;
+      const bool is_y = cls_ok && (int64_t)i == yl;
+      if (is_y) lsum += (double)cw * (double)(-((S - m2) - lse));
+      const float dS = cls_ok ? (q * (1.0f / s2) - (is_y ? 1.0f : 0.0f)) * (cw * scale) : 0.f;
+      const float dot = tr_sum16(dS * S);
+      if (cls_ok && valid) out[row * C + i] = S * (dS - dot);
+    }
+  }
+  if (MODE == MODE_MNL_TRAIN) {
+    lsum = tr_wave_allreduce_d(lsum);
+    if (lane == 0) {
+      dpart[2 * gw] = lsum;
+      dpart[2 * gw + 1] = 0.0;
+    }
+  }
+}
+
+// ==========================================================================================
 // K3 two-pass backward: partial column reduction  Gpart[k][c][p] = sum_{n in chunk k} V[n,c] X[n,p]
 // (the reference's MmBackward0 X^T . dL/dZ).  Workgroup (stripe s, chunk k): 256 threads,
 // each owns CW vectors of columns; the per-row weights V[n, 0..C-1] are wave-uniform scalar
@@ -1000,6 +1142,27 @@ hipError_t launch_rows(int C, int mode, int W, const float* X, int64_t N, int64_
   TR_C_CASES(TR_CALL_ROWS)
 #undef TR_CALL_ROWS
   return hipErrorInvalidValue;
+}
+
+// ---- multinomial forward on MFMA ------------------------------------------------------------
+static const int kMfmaRT = 2;
+bool rows_mfma_supported(int C, int64_t P) { return C >= 1 && C <= 16 && P % 32 == 0; }
+int64_t rows_mfma_num_waves(int64_t N) { return (N + 16 * kMfmaRT - 1) / (16 * kMfmaRT); }
+
+hipError_t launch_rows_mfma(int mode, const float* X, int64_t N, int64_t P, const float* Bt, int C,
+                            const int64_t* lab, const float* class_w, float scale, float* out, double* dpart,
+                            const int32_t* stop, hipStream_t st) {
+  const int64_t waves = rows_mfma_num_waves(N);
+  const unsigned grid = cdiv(waves, 4);
+  if (mode == MODE_MNL_TRAIN)
+    hipLaunchKernelGGL((k_rows_mfma<MODE_MNL_TRAIN, kMfmaRT>), dim3(grid), dim3(256), 0, st, X, N, P, Bt, C, lab,
+                       class_w, scale, out, dpart, stop);
+  else if (mode == MODE_MNL_PRED)
+    hipLaunchKernelGGL((k_rows_mfma<MODE_MNL_PRED, kMfmaRT>), dim3(grid), dim3(256), 0, st, X, N, P, Bt, C, lab,
+                       class_w, scale, out, dpart, stop);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
 }
 
 // ---- two-pass backward columns -------------------------------------------------------------

@@ -31,21 +31,25 @@ RTOL = 1e-5
 
 @contextlib.contextmanager
 def path(kind):
-    """kind: 'auto' (plan's choice, single-pass where eligible) or 'twopass' (forced)."""
+    """kind: 'auto' (plan's choice: single pass / MFMA forward where eligible), 'twopass'
+    (linear: force the two-pass kernels) or 'valu' (multinomial: force the VALU forward)."""
     from tensor_regression_amd import standard_tensor_regression as S
-    old = os.environ.get("TR_FORCE_TWOPASS")
+    saved = {k: os.environ.get(k) for k in ("TR_FORCE_TWOPASS", "TR_NO_MFMA")}
+    for k in saved:
+        os.environ.pop(k, None)
     if kind == "twopass":
         os.environ["TR_FORCE_TWOPASS"] = "1"
-    else:
-        os.environ.pop("TR_FORCE_TWOPASS", None)
+    if kind == "valu":
+        os.environ["TR_NO_MFMA"] = "1"
     S._plan_cache.clear()
     try:
         yield
     finally:
-        if old is None:
-            os.environ.pop("TR_FORCE_TWOPASS", None)
-        else:
-            os.environ["TR_FORCE_TWOPASS"] = old
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
         S._plan_cache.clear()
 
 
@@ -133,8 +137,14 @@ def test_linear_golden(name, kind):
             _assert_factors(model.Bcp, d["Bcp_final2_list"])
 
 
+@pytest.mark.parametrize("kind", ["auto", "valu"])
 @pytest.mark.parametrize("name", MNL)
-def test_multinomial_golden(name):
+def test_multinomial_golden(name, kind):
+    with path(kind):
+        _multinomial_golden(name)
+
+
+def _multinomial_golden(name):
     from tensor_regression_amd import CP_logistic_regression
     from tensor_regression_amd.multinomial_tensor_regression import model as mnl_model
     d = load(name)
@@ -250,11 +260,17 @@ def test_linear_sweep_vs_oracle(shape, rank, kind):
 
 
 MNL_SHAPES = [((50, 8, 4), 2, 2), ((200, 16, 8), 10, 4), ((97, 5, 7), 16, 3), ((64, 33), 3, 1),
-              ((128, 4, 4, 4), 5, 6)]
+              ((128, 4, 4, 4), 5, 6), ((333, 32, 32), 10, 8), ((40, 64), 16, 2), ((3, 32), 3, 2)]
 
 
+@pytest.mark.parametrize("kind", ["auto", "valu"])
 @pytest.mark.parametrize("shape,C,rank", MNL_SHAPES)
-def test_multinomial_sweep_vs_oracle(shape, C, rank):
+def test_multinomial_sweep_vs_oracle(shape, C, rank, kind):
+    with path(kind):
+        _multinomial_sweep(shape, C, rank)
+
+
+def _multinomial_sweep(shape, C, rank):
     from oracle import cp_oracle
     from tensor_regression_amd import CP_logistic_regression
     g = torch.Generator().manual_seed(hash((shape, C, rank)) % 2**31)
