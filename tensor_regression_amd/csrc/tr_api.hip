@@ -124,8 +124,11 @@ static void choose_fused(tr_plan* p) {
   const size_t lds_max = 160 * 1024;
   const int Ts[5] = {64, 128, 256, 512, 1024};
   int64_t best_bytes = 0;
+  int best_waves = 1 << 30;
+  const char* force_t = std::getenv("TR_FUSED_T");  // experiment knob
   for (int k = 0; k < 5; ++k) {
     const int T = Ts[k];
+    if (force_t != nullptr && std::atoi(force_t) != T) continue;
     if (P4 % T != 0) continue;
     const int64_t CH = P4 / T;
     if (!linear_fused_supported(T, (int)CH)) continue;
@@ -134,8 +137,12 @@ static void choose_fused(tr_plan* p) {
     int per_cu = 0;
     if (prepare_linear_fused(T, (int)CH, lds, &per_cu) != hipSuccess || per_cu < 1) continue;
     const int64_t bytes = (int64_t)per_cu * p->P * 4;
-    if (bytes > best_bytes) {
+    const int waves = per_cu * T / 64;
+    // most X bytes in flight per CU; ties -> fewer waves per barrier (with nt loads the
+    // config-2 row streams at 6.80 TB/s with T=512 vs 6.70 with T=1024)
+    if (bytes > best_bytes || (bytes == best_bytes && waves < best_waves)) {
       best_bytes = bytes;
+      best_waves = waves;
       p->fused = 1;
       p->fT = T;
       p->fCH = (int)CH;
