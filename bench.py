@@ -111,6 +111,8 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--time-all-kernels", action="store_true",
+                    help="hipEvent-time every kernel kind (adds per-launch event overhead)")
     ap.add_argument("--traffic", default=os.path.join(HERE, "profiles", "traffic.json"),
                     help="PMC traffic summary (tools/pmc_traffic.py output) for the roofline 'traffic' field")
     args = ap.parse_args()
@@ -120,7 +122,7 @@ def main():
     rank_id = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     pg = None
-    if world > 1:
+    if world > 1 or os.environ.get("TR_BENCH_FORCE_PG") == "1":  # force: exercise RCCL at world 1
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
@@ -153,7 +155,9 @@ def main():
     fit(args.warmup)
     plan = model._plan
     plan.read_timing()
-    plan.set_timing(True)
+    # time only the X-streaming kernels by default (2 events per stream launch): timing every
+    # tail launch adds event packets between kernels and inflates ms_per_step
+    plan.set_timing(True, kinds=None if args.time_all_kernels else ["stream_fused", "stream_rows", "stream_cols"])
 
     def barrier():
         if pg is not None:

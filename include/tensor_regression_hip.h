@@ -151,8 +151,8 @@ int tr_adam_step(tr_plan* plan, float* params, const float* grad, float* exp_avg
 
 /*
  * Per-kernel device timing (measurement support; no reference counterpart).
- * When enabled, every launch of the plan is bracketed by hipEvents on the caller's stream
- * (no host synchronisation).  tr_plan_read_timing synchronises the recorded events and returns,
+ * `enable` is a bit mask over TR_KERNEL_* kinds (1 << kind; -1 = all): every launch of a
+ * selected kind is bracketed by hipEvents on the caller's stream (no host synchronisation).  tr_plan_read_timing synchronises the recorded events and returns,
  * per kernel kind (TR_KERNEL_*), the summed elapsed milliseconds and the number of launches,
  * then clears the record.
  */

@@ -159,8 +159,12 @@ class Plan:
                 for f, shp in enumerate(self.factor_shapes())]
 
     # ---- timing ------------------------------------------------------------------------------
-    def set_timing(self, enable):
-        check(self.lib.tr_plan_set_timing(self.h, 1 if enable else 0), "tr_plan_set_timing")
+    def set_timing(self, enable, kinds=None):
+        """Enable hipEvent timing for the given kernel kinds (names of _lib.KERNEL_KINDS; None = all)."""
+        mask = 0
+        if enable:
+            mask = -1 if kinds is None else sum(1 << _lib.KERNEL_KINDS.index(k) for k in kinds)
+        check(self.lib.tr_plan_set_timing(self.h, mask), "tr_plan_set_timing")
 
     def read_timing(self):
         """{kernel kind: (total_ms, launches)} since the last read (synchronises the events)."""

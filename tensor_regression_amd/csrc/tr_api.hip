@@ -45,7 +45,7 @@ struct tr_plan {
   unsigned parity = 0;
   std::string desc;
   // optional per-kernel event timing (tr_plan_set_timing)
-  int timing = 0;
+  int timing = 0;  // bit mask of timed TR_KERNEL_* kinds
   struct Rec {
     hipEvent_t a, b;
     int kind;
@@ -72,7 +72,7 @@ struct TimedLaunch {
   int kind;
   hipEvent_t a = nullptr;
   TimedLaunch(tr_plan* p_, hipStream_t st_, int kind_) : p(p_), st(st_), kind(kind_) {
-    if (p->timing) {
+    if (p->timing & (1 << kind)) {
       a = take_event(p);
       if (a) (void)hipEventRecord(a, st);
     }
@@ -490,7 +490,7 @@ extern "C" int tr_adam_step(tr_plan* p, float* params, const float* grad, float*
 
 extern "C" int tr_plan_set_timing(tr_plan* p, int enable) {
   if (p == nullptr) return fail(TR_E_ARG, "plan is NULL");
-  p->timing = enable ? 1 : 0;
+  p->timing = enable;  // bit mask over TR_KERNEL_* kinds (any non-zero value enables those bits)
   return 0;
 }
 

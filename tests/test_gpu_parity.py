@@ -393,3 +393,42 @@ def test_kat2_notebook_trace_on_gpu():
     got = np.array(m.loss_running)
     assert len(got) == len(KAT2_TRACE)
     np.testing.assert_allclose(got, KAT2_TRACE, rtol=1e-5)
+
+
+def test_process_group_single_rank_matches_local():
+    """fit_Adam over a 1-rank RCCL process group (the multi-GPU code path: global-N normaliser,
+    per-iteration all-reduce of the gradient arena) reproduces the local fit bit for bit."""
+    import socket
+    import torch.distributed as dist
+    from tensor_regression_amd import CP_linear_regression, CP_logistic_regression
+    if not dist.is_initialized():
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                                device_id=torch.device(DEV))
+    g = torch.Generator().manual_seed(4)
+    X = torch.randn(2048, 32, 16, generator=g).to(DEV)
+    y = torch.randn(2048, generator=g).to(DEV)
+    res = []
+    for pg in (None, dist.group.WORLD):
+        torch.manual_seed(0)
+        m = CP_linear_regression(X.shape, rank=4, device=DEV)
+        m.fit_Adam(X, y, lambda_L2=0.01, max_iter=15, tol=0, patience=10, Adam_kwargs={"lr": 0.01},
+                   process_group=pg)
+        res.append((list(m.loss_running), [a.detach().cpu().numpy() for a in m.Bcp]))
+    assert res[0][0] == res[1][0]
+    for a, b in zip(res[0][1], res[1][1]):
+        assert np.array_equal(a, b)
+    yl = torch.randint(0, 3, (2048,), generator=g)
+    yl[:3] = torch.arange(3)
+    res = []
+    for pg in (None, dist.group.WORLD):
+        torch.manual_seed(0)
+        mm = CP_logistic_regression(X, yl.to(DEV), rank=3, device=DEV)
+        mm.fit_Adam(lambda_L2=0.01, max_iter=10, tol=0, patience=10, weights=np.ones(3), Adam_kwargs={"lr": 0.01},
+                    process_group=pg)
+        res.append(list(mm.loss_running))
+    assert res[0] == res[1]
+    dist.destroy_process_group()
