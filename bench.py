@@ -104,6 +104,10 @@ def cpu_baseline(cfg, X, y, model_init, budget_s=15.0):
 
 
 def main():
+    # exactly ONE line on stdout: route everything else (RCCL's banner, library prints) to stderr
+    json_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
@@ -233,7 +237,8 @@ def main():
     else:
         out["cpu_baseline"] = None
     if rank_id == 0:
-        print(json.dumps(out), flush=True)
+        json_out.write(json.dumps(out) + "\n")
+        json_out.flush()
     if pg is not None:
         torch.distributed.destroy_process_group()
 
