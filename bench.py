@@ -195,6 +195,8 @@ def main():
         dom = "stream_rows" if kt["stream_rows"][0] >= kt["stream_cols"][0] else "stream_cols"
         bytes_launch = N * P * 4 + N * 4 * (cfg.get("classes", 1))
         dom_name = "k_rows" if dom == "stream_rows" else "k_cols"
+        if dom == "stream_rows" and "+mfma-fwd" in plan.describe:
+            dom_name = "k_rows_mfma"
     dom_ms = kernel_avg[dom]
     achieved = bytes_launch / (dom_ms * 1e-3) / 1e9
     traffic = None

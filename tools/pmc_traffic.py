@@ -15,7 +15,7 @@ import json
 import os
 import re
 
-KERNELS = {"k_linear_fused": r"k_linear_fused", "k_rows": r"k_rows<", "k_cols": r"k_cols<",
+KERNELS = {"k_linear_fused": r"k_linear_fused", "k_rows": r"k_rows<", "k_rows_mfma": r"k_rows_mfma<", "k_cols": r"k_cols<",
            "k_reduce_slabs": r"k_reduce_slabs", "k_mttkrp": r"k_mttkrp", "k_update": r"k_update"}
 
 
@@ -38,7 +38,8 @@ def main():
     ap.add_argument("--write", required=True)
     ap.add_argument("--out", default=os.path.join(os.path.dirname(__file__), "..", "profiles", "traffic.json"))
     ap.add_argument("--algorithmic", type=float, default=None,
-                    help="algorithmic bytes per launch of k_linear_fused (for the ratio column)")
+                    help="algorithmic bytes per launch of the dominant kernel (for the ratio column)")
+    ap.add_argument("--dominant", default="k_linear_fused")
     args = ap.parse_args()
     fetch, nf = per_kernel(args.fetch, "FETCH_SIZE")
     write, nw = per_kernel(args.write, "WRITE_SIZE")
@@ -52,8 +53,9 @@ def main():
             ent["read_bytes_per_launch"] = 2.0 * fkb * 1024.0
             ent["write_bytes_per_launch"] = wkb * 1024.0
         res[k] = ent
-    if args.algorithmic and "k_linear_fused" in res and "hbm_bytes_per_launch" in res["k_linear_fused"]:
-        res["k_linear_fused"]["traffic_over_algorithmic"] = res["k_linear_fused"]["hbm_bytes_per_launch"] / args.algorithmic
+    dom = args.dominant
+    if args.algorithmic and dom in res and "hbm_bytes_per_launch" in res[dom]:
+        res[dom]["traffic_over_algorithmic"] = res[dom]["hbm_bytes_per_launch"] / args.algorithmic
     res["_method"] = ("rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; hbm bytes = "
                       "(2*FETCH_SIZE + WRITE_SIZE)*1024 (gfx950 FETCH_SIZE half-count correction)")
     out = {}
