@@ -49,3 +49,21 @@ def normwise_rel(a, b):
     b = np.asarray(b, dtype=np.float64)
     den = np.linalg.norm(b.ravel())
     return float(np.linalg.norm((a - b).ravel()) / (den if den > 0 else 1.0))
+
+
+def load_spectral(name):
+    """Spectral fixture: factor lists Bcp_n (I, Rn, 1) and Bcp_c (W, Rs, Cc), (D, Rs, 1), (n_out, Rs, 1)."""
+    d = dict(np.load(os.path.join(GOLDEN, name + ".npz")))
+    meta = json.loads(str(d.pop("meta")))
+    sn = [tuple(s) for s in meta["factor_shapes_n"]]
+    sc = [tuple(s) for s in meta["factor_shapes_c"]]
+    d["X"] = torch.tensor(d["X_q"].astype(np.float32) / 8.0)
+    for key in ("Bcp_n0", "Bcp_n_10", "Bcp_n_final", "grads_n0"):
+        if key in d:
+            d[key + "_list"] = split(d[key], sn) if d[key].size else [np.zeros(s, np.float32) for s in sn]
+    for key in ("Bcp_c0", "Bcp_c_10", "Bcp_c_final", "grads_c0"):
+        if key in d:
+            d[key + "_list"] = split(d[key], sc) if d[key].size else [np.zeros(s, np.float32) for s in sc]
+    d["meta"] = meta
+    d["shapes_n"], d["shapes_c"] = sn, sc
+    return d

@@ -29,6 +29,7 @@ sys.dont_write_bytecode = True
 
 import standard_tensor_regression as STR  # noqa: E402  (reference)
 import multinomial_tensor_regression as MTR  # noqa: E402  (reference)
+import spectral_tensor_regression as SPR  # noqa: E402  (reference)
 
 OUT = os.path.join(REPO, "tests", "golden")
 
@@ -148,6 +149,69 @@ def mnl_case(name, seed, shape, n_classes, rank, non_negative, class_w, lam, ada
          loss_running_10=np.array(m10.loss_running), meta=np.array(json.dumps(meta)))
 
 
+def _flat(ts):
+    ts = [t.detach().numpy() if isinstance(t, torch.Tensor) else t for t in ts]
+    return np.concatenate([t.reshape(-1) for t in ts]) if ts else np.zeros(0, np.float32)
+
+
+def spectral_case(name, seed, shape, n_out, rank_normal, rank_spectral, n_complex_dim, non_negative, lam,
+                  adam_kwargs, iters, tol=0.0, patience=10, softplus=None, nan_y=False, lbfgs_kwargs=None,
+                  logging_interval=1):
+    """spectral_tensor_regression.CP_linear_regression: one forward/loss/backward at the init point
+    (fit model = lin_model + stepwise_spectral_model, spectral…py:716-720), predict (spectral_model,
+    :959-960), a 10-iteration and a full fit_Adam run (or LBFGS fit when lbfgs_kwargs is given)."""
+    rng = np.random.default_rng(seed)
+    Xq, X = exact_X(rng, shape)
+    y = torch.tensor(rng.standard_normal((shape[0], n_out)).astype(np.float32))
+    if nan_y:
+        y[3, 0] = float("nan")
+
+    def make():
+        torch.manual_seed(seed)
+        return SPR.CP_linear_regression(X.shape, y.shape, rank_normal=rank_normal, rank_spectral=rank_spectral,
+                                        non_negative=non_negative, n_complex_dim=n_complex_dim,
+                                        softplus_kwargs=softplus)
+
+    m = make()
+    Bn0, Bc0 = _flat(m.Bcp_n), _flat(m.Bcp_c)
+    w = m.weights
+    y_hat = (SPR.lin_model(X, m.Bcp_n, w[:m.rank_normal], m.non_negative, m.bias, softplus_kwargs=m.softplus_kwargs) +
+             SPR.stepwise_spectral_model(X, m.Bcp_c, w[m.rank_normal:], m.non_negative, m.bias,
+                                         softplus_kwargs=m.softplus_kwargs))
+    loss = torch.nn.MSELoss()(y_hat, y) + lam * (SPR.L2_penalty(m.Bcp_n) + SPR.L2_penalty(m.Bcp_c))
+    loss.backward()
+    gn = _flat([A.grad for A in m.Bcp_n if A.grad is not None]) if rank_normal else np.zeros(0, np.float32)
+    gc_ = _flat([A.grad for A in m.Bcp_c if A.grad is not None]) if rank_spectral else np.zeros(0, np.float32)
+    bg = m.bias.grad.numpy().copy()
+    pred0 = m.predict(X).numpy()
+    out = dict(X_q=Xq, y=y.numpy(), Bcp_n0=Bn0, Bcp_c0=Bc0, y_hat0=y_hat.detach().numpy(),
+               loss0=np.float64(loss.item()), grads_n0=gn, grads_c0=gc_, bias_grad0=bg, predict0=pred0)
+    if lbfgs_kwargs is None:
+        m10 = make()
+        m10.fit_Adam(X, y, lambda_L2=lam, max_iter=min(10, iters), tol=tol, patience=patience, verbose=False,
+                     Adam_kwargs=dict(adam_kwargs))
+        out.update(Bcp_n_10=_flat(m10.Bcp_n), Bcp_c_10=_flat(m10.Bcp_c), bias_10=m10.bias.detach().numpy().copy(),
+                   loss_running_10=np.array(m10.loss_running, dtype=np.float64))
+        m = make()
+        conv = m.fit_Adam(X, y, lambda_L2=lam, max_iter=iters, tol=tol, patience=patience, verbose=False,
+                          Adam_kwargs=dict(adam_kwargs))
+    else:
+        m = make()
+        conv = m.fit(X, y, lambda_L2=lam, max_iter=iters, tol=tol, patience=patience, verbose=False,
+                     running_loss_logging_interval=logging_interval, LBFGS_kwargs=dict(lbfgs_kwargs))
+    out.update(loss_running=np.array(m.loss_running, dtype=np.float64), Bcp_n_final=_flat(m.Bcp_n),
+               Bcp_c_final=_flat(m.Bcp_c), bias_final=m.bias.detach().numpy().copy(), converged=np.int32(conv),
+               predict_final=m.predict(X).numpy())
+    meta = dict(model="spectral", seed=seed, shape=list(shape), n_out=n_out, rank_normal=rank_normal,
+                rank_spectral=rank_spectral, n_complex_dim=n_complex_dim, non_negative=m.non_negative,
+                lambda_L2=lam, adam_kwargs=adam_kwargs, lbfgs_kwargs=lbfgs_kwargs, logging_interval=logging_interval,
+                max_iter=iters, tol=tol, patience=patience, softplus_kwargs=m.softplus_kwargs, nan_y=nan_y,
+                factor_shapes_n=[list(a.shape) for a in m.Bcp_n], factor_shapes_c=[list(a.shape) for a in m.Bcp_c],
+                torch=torch.__version__)
+    out["meta"] = np.array(json.dumps(meta))
+    save(name, **out)
+
+
 def init_case(name):
     """make_BcpInit RNG parity: the reference's initialisers for fixed seeds."""
     out = {}
@@ -198,9 +262,17 @@ def kat_replay():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--kat", action="store_true")
+    ap.add_argument("--only", default=None, help="generate only the cases whose name starts with this prefix")
     args = ap.parse_args()
     os.makedirs(OUT, exist_ok=True)
     torch.set_num_threads(1)  # fixed summation order for the golden outputs
+    if args.only:
+        global save
+        _save = save
+
+        def save(name, **arrays):  # noqa: F811
+            if name.startswith(args.only):
+                _save(name, **arrays)
     adam = {'lr': 0.01}
     linear_case("lin_basic", 11, (64, 8, 4), 2, [False, False, False], 0.3, 0.01, adam, 50)
     linear_case("lin_nonneg_amsgrad_wd", 12, (96, 12, 8), 3, [True, False, True], -0.2, 0.05,
@@ -222,6 +294,20 @@ def main():
     mnl_case("mnl_converge", 24, (96, 4, 4), 2, 2, [False, False, False], [1, 1], 0.01, {'lr': 0.001}, 300,
              tol=0.01, patience=5)
     init_case("init_rng")
+    spectral_case("spec_basic", 31, (64, 12, 9), 3, 2, 2, 1, False, 0.01, adam, 50)
+    spectral_case("spec_nonneg_amsgrad_wd", 32, (80, 16, 17), 2, 3, 2, 2, [True, False, True], 0.02,
+                  {'lr': 0.02, 'amsgrad': True, 'weight_decay': 0.01, 'betas': (0.8, 0.99), 'eps': 1e-6}, 50)
+    spectral_case("spec_c5_shape", 33, (128, 32, 33), 2, 8, 8, 1, False, 0.01, adam, 40)
+    spectral_case("spec_rn0", 34, (48, 8, 5), 2, 0, 3, 1, False, 0.01, adam, 30)
+    spectral_case("spec_rs0", 35, (48, 8, 5), 2, 3, 0, 1, False, 0.01, adam, 30)
+    spectral_case("spec_cc1_softplus", 36, (40, 6, 7), 4, 2, 3, 0, [True, True, True], 0.01, adam, 30,
+                  softplus={'beta': 5, 'threshold': 2})
+    spectral_case("spec_converge", 37, (64, 8, 5), 2, 2, 2, 1, False, 0.01, {'lr': 0.001}, 400, tol=0.02,
+                  patience=5)
+    spectral_case("spec_nan", 38, (32, 6, 5), 2, 2, 2, 1, False, 0.01, adam, 20, nan_y=True)
+    spectral_case("spec_lbfgs", 39, (64, 8, 5), 2, 2, 2, 1, False, 1e-3, None, 5, tol=0.0, patience=100,
+                  lbfgs_kwargs={'lr': 1, 'max_iter': 20, 'max_eval': None, 'tolerance_grad': 1e-07,
+                                'tolerance_change': 1e-09, 'history_size': 100, 'line_search_fn': "strong_wolfe"})
     if args.kat:
         kat_replay()
 
