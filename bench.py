@@ -42,7 +42,12 @@ CONFIGS = {
     "c4": dict(kind="linear", rows=16384, dims=(64, 64, 32), rank=16,
                workload="configs[3]: 4-D CP regression, X (131072, 64, 64, 32) sharded 16384 samples per GPU, "
                         "rank 16, Adam lr 0.01"),
+    "c5": dict(kind="spectral", rows=32768, dims=(256, 129), rank=8, rank_spectral=8, n_complex_dim=1, n_out=2,
+               workload="configs[4]: spectral_tensor_regression.py fit_Adam, X (32768, 256, 129) fp32 (real: the "
+                        "reference rejects complex X; |rfft|-like non-negative synthetic data), rank_normal = "
+                        "rank_spectral = 8, n_complex_dim 1, y (32768, 2), Adam lr 0.01"),
 }
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32 = the fp32 vector rate
 
 
 def log(*a):
@@ -55,6 +60,14 @@ def make_data(cfg, rank_id, dev):
     N, dims, R = cfg["rows"], cfg["dims"], cfg["rank"]
     X = torch.randn((N,) + tuple(dims), device=dev, generator=g, dtype=torch.float32)
     gc = torch.Generator().manual_seed(99)  # planted factors identical on every rank
+    if cfg["kind"] == "spectral":
+        from tensor_regression_amd.spectral_tensor_regression import lin_model as spec_lin
+        X.abs_()  # magnitude-spectrum-like (non-negative) features
+        O = cfg["n_out"]
+        A = [(torch.randn(d, R, 1, generator=gc) / 8).to(dev) for d in dims] + [torch.randn(O, R, 1, generator=gc).to(dev)]
+        y = spec_lin(X, A, torch.ones(R, device=dev), [False] * 3, torch.zeros(O, device=dev))
+        y = y + 0.1 * torch.randn(N, O, device=dev, generator=g)
+        return X, y
     if cfg["kind"] == "linear":
         from tensor_regression_amd.standard_tensor_regression import lin_model
         A = [(torch.randn(d, R, generator=gc) / 4).to(dev) for d in dims]
@@ -80,6 +93,10 @@ def cpu_baseline(cfg, X, y, model_init, budget_s=15.0):
     lam, adam = 0.01, {"lr": 0.01}
 
     def run(iters):
+        if cfg["kind"] == "spectral":
+            return cp_oracle.fit_adam_spectral(Xc, yc, model_init[0], model_init[1], np.zeros(cfg["n_out"], np.float32),
+                                               np.ones(R + cfg["rank_spectral"], np.float32), R, [False] * 3, lam,
+                                               iters, 0.0, 10, adam)
         if cfg["kind"] == "linear":
             return cp_oracle.fit_adam_linear(Xc, yc, model_init[0], model_init[1], np.ones(R, np.float32),
                                              [False] * len(cfg["dims"]), lam, iters, 0.0, 10, adam)
@@ -140,7 +157,17 @@ def main():
     torch.cuda.synchronize()
     R = cfg["rank"]
     torch.manual_seed(1)
-    if cfg["kind"] == "linear":
+    if cfg["kind"] == "spectral":
+        from tensor_regression_amd.spectral_tensor_regression import CP_linear_regression as SpectralCP
+        model = SpectralCP(X.shape, y.shape, rank_normal=R, rank_spectral=cfg["rank_spectral"],
+                           n_complex_dim=cfg["n_complex_dim"], device=dev)
+        init = ([a.detach().cpu().numpy().copy() for a in model.Bcp_n],
+                [a.detach().cpu().numpy().copy() for a in model.Bcp_c])
+
+        def fit(iters):
+            return model.fit_Adam(X, y, lambda_L2=0.01, max_iter=iters, tol=0, patience=10,
+                                  Adam_kwargs={"lr": 0.01}, process_group=pg)
+    elif cfg["kind"] == "linear":
         model = CP_linear_regression(X.shape, rank=R, device=dev)
         init = ([a.detach().cpu().numpy().copy() for a in model.Bcp], model.bias.detach().cpu().numpy().copy())
 
@@ -187,7 +214,14 @@ def main():
 
     stream_kinds = ["stream_fused"] if kt["stream_fused"][1] else ["stream_rows", "stream_cols"]
     kernel_avg = {k: (v[0] / v[1] if v[1] else None) for k, v in kt.items()}
-    if kt["stream_fused"][1]:
+    flops_launch = None
+    if cfg["kind"] == "spectral":
+        dom = "stream_fused"
+        bytes_launch = N * P * 4 + N * 4 * cfg["n_out"]
+        # fwd GEMM X_n^T Phi0 + bwd GEMM X_n dT_n: 2 * 2*W*D*K flops per sample
+        flops_launch = 4 * N * P * (R + cfg["rank_spectral"] * (cfg["n_complex_dim"] + 1))
+        dom_name = "k_spec_fused"
+    elif kt["stream_fused"][1]:
         dom = "stream_fused"
         bytes_launch = N * P * 4 + N * 4
         dom_name = "k_linear_fused"
@@ -233,6 +267,16 @@ def main():
                      "kernel_avg_ms": dom_ms, "algorithmic_bytes_per_launch": bytes_launch},
         "kernel_avg_ms": kernel_avg,
     }
+    if flops_launch is not None:
+        # spectral: 4*W*D*K flops per 4*W*D-byte sample = K = 24 flop/B > the fp32 ridge
+        # 157.3 TF / 8 TB/s = 19.7 flop/B, so the algorithmic bound is the fp32 matrix rate
+        tflops = flops_launch / (dom_ms * 1e-3) / 1e12
+        out["roofline"] = {"bound": "mfma", "kernel": dom_name, "achieved": tflops, "peak": FP32_MFMA_PEAK_TFLOPS,
+                           "unit": "TFLOP/s", "frac": tflops / FP32_MFMA_PEAK_TFLOPS, "traffic": traffic,
+                           "kernel_avg_ms": dom_ms, "algorithmic_flops_per_launch": flops_launch,
+                           "algorithmic_bytes_per_launch": bytes_launch, "hbm_GBps": achieved,
+                           "hbm_frac": achieved / HBM_PEAK_GBPS}
+        out["dtype"] = "fp32"
     if rank_id == 0 and world == 1 and not args.no_cpu_baseline:
         log("cpu baseline ...")
         out["cpu_baseline"] = cpu_baseline(cfg, X, y, init, args.cpu_budget)

@@ -46,10 +46,11 @@
 extern "C" {
 #endif
 
-#define TR_ABI_VERSION 1
+#define TR_ABI_VERSION 2
 
 #define TR_MODEL_LINEAR 0      /* CP_linear_regression: y_hat = <X, [[w; Phi]]> + bias, MSE */
 #define TR_MODEL_MULTINOMIAL 1 /* CP_logistic_regression: softmax(<X, [[w; Phi]]>), CE(weight) */
+#define TR_MODEL_SPECTRAL 2    /* spectral CP_linear_regression: lin_model + stepwise_spectral_model, MSE */
 
 #define TR_MAX_FACTORS 8
 
@@ -148,6 +149,38 @@ int tr_adam_step(tr_plan* plan, float* params, const float* grad, float* exp_avg
                  double beta1, double beta2, double eps, double weight_decay, int amsgrad,
                  int64_t step, double* loss_hist, int64_t hist_base, int64_t iter,
                  int64_t patience, double tol, int32_t* stop_flag, void* stream);
+
+/*
+ * Spectral model plan (spectral_tensor_regression.CP_linear_regression, spectral…py:424-539;
+ * fit model lin_model :118-165 + stepwise_spectral_model :339-390; predict model
+ * lin_model + spectral_model :168-220).  X is (N, n_w, n_d) fp32, y is (N, n_out) fp32.
+ *   n_complex      = n_complex_dim + 1 (third dim of Bcp_c[0])
+ *   non_negative   host int32[3]: flags of the (w, d, out) factors, shared by Bcp_n and Bcp_c
+ * Parameter arena (reference order Bcp_n + Bcp_c + [bias], each row-major):
+ *   A0 (n_w, Rn) | A1 (n_d, Rn) | A2 (n_out, Rn) | C0 (n_w, Rs, n_complex) | C1 (n_d, Rs) |
+ *   C2 (n_out, Rs) | bias (n_out)
+ * tr_plan_factor_offset(plan, f) gives f = 0..5 and the bias offset for f = 6.
+ * With such a plan:
+ *   tr_loss_grad   target = y (N x n_out floats), norm = global N * n_out (MSELoss mean),
+ *                  class_weight = NULL, yhat_out (optional) = fit-model y_hat (N x n_out)
+ *   tr_forward     out (N x n_out) = the reference's predict() model (spectral…py:959-960);
+ *                  weights = all rank_normal + rank_spectral weights
+ *   tr_adam_step   also applies the spectral NaN stop (spectral…py:738-741): when the loss
+ *                  is NaN and iter <= patience, *stop_flag = -(iter + 1) (stopped, not converged)
+ * Envelope of the gfx950 kernel: n_w, n_d <= 256, n_out <= 256, Rn + Rs*n_complex <= 32, one
+ * sample (n_w * n_d floats) plus scratch within the 160 KiB LDS of a CU; TR_E_UNSUPPORTED
+ * otherwise.
+ */
+int tr_plan_create_spectral(tr_plan** out, int device, int64_t n_w, int64_t n_d, int64_t n_out,
+                            int rank_normal, int rank_spectral, int n_complex, int64_t max_rows,
+                            const int32_t* non_negative, float softplus_beta, float softplus_threshold);
+
+/*
+ * stepwise_latents_model (spectral…py:284-336) — out (N x rank_normal) =
+ * einsum('tdr,drs->tr', einsum('twd,wrs->tdr', X, phi(A0)), phi(A1)); used by predict_latents.
+ */
+int tr_spectral_latents(tr_plan* plan, const float* X, int64_t n_rows, const float* params, float* out,
+                        void* stream);
 
 /*
  * Per-kernel device timing (measurement support; no reference counterpart).

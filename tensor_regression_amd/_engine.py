@@ -205,6 +205,79 @@ class Plan:
         check(rc, "tr_adam_step")
 
 
+class SpectralPlan(Plan):
+    """`tr_plan` of the spectral model (spectral_tensor_regression.CP_linear_regression):
+    arena = Bcp_n (3 factors (I, Rn, 1)) + Bcp_c (3 factors, the first (W, Rs, Cc)) + bias (n_out)."""
+
+    def __init__(self, n_w, n_d, n_out, rank_normal, rank_spectral, n_complex, max_rows, non_negative,
+                 softplus_kwargs, device):
+        self.lib = _lib.load()
+        self.dev = device_index(device)
+        self.device_str = f"cuda:{self.dev}"
+        self.model = _lib.TR_MODEL_SPECTRAL
+        self.dims = (int(n_w), int(n_d), int(n_out))
+        self.rank_normal, self.rank_spectral, self.n_complex = int(rank_normal), int(rank_spectral), int(n_complex)
+        self.max_rows = int(max_rows)
+        self.n_factors = 6
+        nn = (ctypes.c_int32 * 3)(*[1 if bool(non_negative[f]) else 0 for f in range(3)])
+        beta, thr = softplus_params(softplus_kwargs)
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.dev):
+            rc = self.lib.tr_plan_create_spectral(ctypes.byref(h), self.dev, self.dims[0], self.dims[1], self.dims[2],
+                                                  self.rank_normal, self.rank_spectral, self.n_complex,
+                                                  max(1, self.max_rows), nn, beta, thr)
+        check(rc, "tr_plan_create_spectral")
+        self.h = h
+        self.num_params = int(self.lib.tr_plan_num_params(h))
+        self.num_grads = int(self.lib.tr_plan_num_grads(h))
+        self.offsets = [int(self.lib.tr_plan_factor_offset(h, f)) for f in range(7)]
+        self.describe = self.lib.tr_plan_describe(h).decode()
+
+    def factor_shapes(self):
+        W, D, O = self.dims
+        Rn, Rs, Cc = self.rank_normal, self.rank_spectral, self.n_complex
+        return [(W, Rn, 1), (D, Rn, 1), (O, Rn, 1), (W, Rs, Cc), (D, Rs, 1), (O, Rs, 1)]
+
+    def pack(self, Bcp_n, Bcp_c, bias):
+        arena = torch.empty(self.num_params, dtype=torch.float32, device=self.device_str)
+        shapes = self.factor_shapes()
+        facs = list(Bcp_n) + list(Bcp_c)
+        if len(facs) != 6:
+            raise ValueError(f"expected 3 + 3 Kruskal factors, got {len(Bcp_n)} + {len(Bcp_c)}")
+        with torch.no_grad():
+            for f, (A, shp) in enumerate(zip(facs, shapes)):
+                A = torch.as_tensor(A)
+                if tuple(A.shape) != shp:
+                    raise ValueError(f"factor {f} has shape {tuple(A.shape)}, expected {shp}")
+                arena[self.offsets[f]:self.offsets[f + 1]].copy_(A.detach().reshape(-1))
+            arena[self.offsets[6]:].copy_(torch.as_tensor(bias).detach().reshape(-1))
+        return arena
+
+    def unpack_into(self, arena, Bcp_n, Bcp_c, bias=None):
+        with torch.no_grad():
+            for f, A in enumerate(list(Bcp_n) + list(Bcp_c)):
+                A.copy_(arena[self.offsets[f]:self.offsets[f + 1]].view(A.shape).to(device=A.device, dtype=A.dtype))
+            if bias is not None:
+                bias.copy_(arena[self.offsets[6]:].to(device=bias.device, dtype=bias.dtype).view(bias.shape))
+
+    def forward(self, X, arena, weights, out=None):
+        """The reference's predict model: lin_model + spectral_model (N, n_out)."""
+        if out is None:
+            out = torch.empty((X.shape[0], self.dims[2]), dtype=torch.float32, device=X.device)
+        rc = self.lib.tr_forward(self.h, ptr(X), X.shape[0], ptr(arena), ptr(weights), ptr(out),
+                                 stream_handle(self.dev))
+        check(rc, "tr_forward")
+        return out
+
+    def latents(self, X, arena, out=None):
+        """stepwise_latents_model (N, rank_normal)."""
+        if out is None:
+            out = torch.zeros((X.shape[0], self.rank_normal), dtype=torch.float32, device=X.device)
+        rc = self.lib.tr_spectral_latents(self.h, ptr(X), X.shape[0], ptr(arena), ptr(out), stream_handle(self.dev))
+        check(rc, "tr_spectral_latents")
+        return out
+
+
 def as_device_f32(X, dev):
     """X as a contiguous fp32 tensor on cuda:dev (copies only when needed)."""
     if not isinstance(X, torch.Tensor):
@@ -255,6 +328,8 @@ def run_adam_fit(plan, X, target, class_weight, norm, arena, weights, lambda_L2,
             verbose_cb.after_step(ii - 1, float(hist[base + ii - 1].item()))
         if stopped_at:
             break
-    n_run = stopped_at if stopped_at else ii
+    # stop flag: > 0 plateau convergence after that many iterations; < 0 NaN stop (spectral)
+    n_run = abs(stopped_at) if stopped_at else ii
     loss_running.extend(hist[base:base + n_run].tolist())
-    return bool(stopped_at), n_run
+    plan.last_stop = stopped_at
+    return stopped_at > 0, n_run

@@ -12,9 +12,10 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TR_HIP_LIB", os.path.join(_HERE, "libtr_hip.so"))
 
-TR_ABI_VERSION = 1
+TR_ABI_VERSION = 2
 TR_MODEL_LINEAR = 0
 TR_MODEL_MULTINOMIAL = 1
+TR_MODEL_SPECTRAL = 2
 TR_MAX_FACTORS = 8
 KERNEL_KINDS = ["stream_fused", "stream_rows", "stream_cols", "reduce", "mttkrp", "prep", "update"]
 
@@ -38,6 +39,10 @@ SIGNATURES = {
     "tr_finalize_grad": (_c.c_int, [_vp, _vp, _vp, _c.c_float, _vp, _vp, _vp]),
     "tr_plan_set_timing": (_c.c_int, [_vp, _c.c_int]),
     "tr_plan_read_timing": (_c.c_int, [_vp, _c.POINTER(_c.c_double), _c.POINTER(_c.c_int64)]),
+    "tr_plan_create_spectral": (_c.c_int, [_c.POINTER(_vp), _c.c_int, _c.c_int64, _c.c_int64, _c.c_int64, _c.c_int,
+                                           _c.c_int, _c.c_int, _c.c_int64, _c.POINTER(_c.c_int32), _c.c_float,
+                                           _c.c_float]),
+    "tr_spectral_latents": (_c.c_int, [_vp, _vp, _c.c_int64, _vp, _vp, _vp]),
     "tr_adam_step": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _c.c_float, _c.c_double, _c.c_double,
                                 _c.c_double, _c.c_double, _c.c_double, _c.c_int, _c.c_int64, _vp,
                                 _c.c_int64, _c.c_int64, _c.c_int64, _c.c_double, _vp, _vp]),

@@ -16,6 +16,7 @@
 
 #include "../../include/tensor_regression_hip.h"
 #include "tr_kernels.h"
+#include "tr_spectral.h"
 
 using namespace tr;
 
@@ -34,6 +35,11 @@ struct tr_plan {
   // single-pass linear strategy
   int fused = 0, fT = 0, fCH = 0, fgrid = 0;
   int mfma_rows = 0;  // multinomial forward on the matrix cores
+  // spectral model (TR_MODEL_SPECTRAL)
+  SpecGeom sg{};
+  float* Phi0 = nullptr;
+  int sgrid = 0;
+  int64_t slab_stride = 0;
   // two-pass strategy
   int64_t max_slabs = 0;
   // workspace
@@ -301,6 +307,110 @@ extern "C" int tr_plan_create(tr_plan** out, int device, int model, int n_featur
   return 0;
 }
 
+// Spectral plan (spectral_tensor_regression.CP_linear_regression.__init__, :425-539): the
+// parameter arena is Bcp_n + Bcp_c + [bias] in the reference's order; the per-iteration
+// pipeline is prep -> fused single pass -> slab reduction -> softplus chain.
+extern "C" int tr_plan_create_spectral(tr_plan** out, int device, int64_t n_w, int64_t n_d, int64_t n_out,
+                                       int rank_normal, int rank_spectral, int n_complex, int64_t max_rows,
+                                       const int32_t* non_negative, float softplus_beta,
+                                       float softplus_threshold) {
+  if (out == nullptr) return fail(TR_E_ARG, "out is NULL");
+  *out = nullptr;
+  if (max_rows < 1) return fail(TR_E_ARG, "max_rows must be >= 1");
+  if (n_w < 1 || n_d < 1 || n_out < 1 || rank_normal < 0 || rank_spectral < 0 || n_complex < 1)
+    return fail(TR_E_ARG, "spectral dims / ranks out of range");
+  if (rank_normal + rank_spectral < 1) return fail(TR_E_ARG, "rank_normal + rank_spectral must be >= 1");
+  tr_plan* p = new tr_plan();
+  std::string why;
+  if (!spec_geom_init(&p->sg, n_w, n_d, n_out, rank_normal, rank_spectral, n_complex, non_negative, &why)) {
+    delete p;
+    return fail(TR_E_UNSUPPORTED, why);
+  }
+  const SpecGeom& g = p->sg;
+  p->device = device;
+  p->model = TR_MODEL_SPECTRAL;
+  p->K = 2;
+  p->C = (int)n_out;
+  p->R = rank_normal + rank_spectral;
+  p->has_bias = (int)n_out;  // bias entries (one per output)
+  p->sp_beta = softplus_beta;
+  p->sp_thr = softplus_threshold;
+  p->max_rows = max_rows;
+  p->P = g.WD;
+  p->nparams = g.nparams;
+  p->ngrads = g.nparams + 1;
+  FactorSet& fs = p->fs;
+  std::memset(&fs, 0, sizeof(fs));
+  fs.nf = 6;
+  fs.rank = 0;
+  const int64_t offs[6] = {g.offA0, g.offA1, g.offA2, g.offC0, g.offC1, g.offC2};
+  const int64_t dims[6] = {n_w, n_d, n_out, n_w, n_d, n_out};
+  for (int f = 0; f < 6; ++f) {
+    fs.off[f] = offs[f];
+    fs.dim[f] = dims[f];
+    fs.nonneg[f] = g.nonneg[f % 3];
+  }
+  fs.nfelem = g.offB;
+  fs.total = 0;
+
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) {
+    delete p;
+    return hip_fail(e, "hipSetDevice");
+  }
+  int ncu = 0;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
+    p->ncu = ncu;
+  for (int mode = SPEC_TRAIN; mode <= SPEC_LATENT; ++mode) {
+    int ok = 0;
+    e = spec_prepare(g, mode, &ok);
+    if (e != hipSuccess) {
+      delete p;
+      return hip_fail(e, "spec_prepare");
+    }
+    if (!ok) {
+      delete p;
+      return fail(TR_E_UNSUPPORTED, "spectral kernel does not fit a CU for this shape");
+    }
+  }
+  p->sgrid = p->ncu;  // one workgroup per CU (the kernel holds one sample in 150 KiB of LDS)
+  p->slab_stride = (g.nparams + 3) & ~(int64_t)3;
+  p->gpart_slabs = p->sgrid;
+  p->dpart_n = p->sgrid;
+  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  const size_t b_par = al((size_t)g.nparams * 4), b_phi0 = al((size_t)g.W * g.K * 4),
+               b_G = al((size_t)p->slab_stride * 4), b_gpart = al((size_t)p->sgrid * p->slab_stride * 4),
+               b_dpart = al((size_t)p->dpart_n * 2 * 8);
+  p->ws_bytes = 2 * b_par + b_phi0 + b_G + b_gpart + b_dpart;
+  e = hipMalloc(&p->ws, p->ws_bytes);
+  if (e != hipSuccess) {
+    delete p;
+    return hip_fail(e, "hipMalloc(workspace)");
+  }
+  char* c = (char*)p->ws;
+  p->phi = (float*)c;
+  c += b_par;
+  p->dphi = (float*)c;
+  c += b_par;
+  p->Phi0 = (float*)c;
+  c += b_phi0;
+  p->G = (float*)c;
+  c += b_G;
+  p->gpart = (float*)c;
+  c += b_gpart;
+  p->dpart = (double*)c;
+  TR_HIP(hipMemset(p->ws, 0, p->ws_bytes));
+  char buf[512];
+  std::snprintf(buf, sizeof(buf),
+                "model=spectral W=%d D=%d n_out=%d Rn=%d Rs=%d Cc=%d K=%d nparams=%lld ncu=%d path=fused-1pass-mfma "
+                "KT=%d S=%d grid=%d lds=%.1fKiB vec=%d workspace=%.1fMiB",
+                g.W, g.D, g.NO, g.Rn, g.Rs, g.Cc, g.K, (long long)g.nparams, p->ncu, g.KT, g.S, p->sgrid,
+                g.lds_floats * 4 / 1024.0, g.vec, p->ws_bytes / 1048576.0);
+  p->desc = buf;
+  *out = p;
+  return 0;
+}
+
 extern "C" int tr_plan_destroy(tr_plan* p) {
   if (p == nullptr) return 0;
   (void)hipSetDevice(p->device);
@@ -329,6 +439,29 @@ static int factor_prep(tr_plan* p, const float* params, const float* w, const in
   return 0;
 }
 
+static int spectral_forward(tr_plan* p, int mode, const float* X, int64_t n_rows, const float* params,
+                            const float* weights, float* out, hipStream_t st) {
+  {
+    TimedLaunch tl(p, st, TR_KERNEL_PREP);
+    TR_HIP(launch_spec_prep(p->sg, params, p->sp_beta, p->sp_thr, p->phi, p->dphi, p->Phi0, nullptr, st));
+  }
+  const int64_t rpw = (n_rows + p->sgrid - 1) / p->sgrid;
+  TimedLaunch tl(p, st, TR_KERNEL_STREAM_FUSED);
+  TR_HIP(launch_spec_fused(mode, p->sg, p->sgrid, X, n_rows, p->phi, p->Phi0, weights, nullptr, 0.f, nullptr, 0,
+                           nullptr, out, rpw, 0, nullptr, st));
+  return 0;
+}
+
+extern "C" int tr_spectral_latents(tr_plan* p, const float* X, int64_t n_rows, const float* params, float* out,
+                                   void* stream) {
+  if (p == nullptr) return fail(TR_E_ARG, "plan is NULL");
+  if (p->model != TR_MODEL_SPECTRAL) return fail(TR_E_ARG, "tr_spectral_latents needs a spectral plan");
+  if (X == nullptr || params == nullptr || out == nullptr) return fail(TR_E_ARG, "NULL buffer");
+  if (n_rows < 1 || p->sg.Rn < 1) return 0;
+  TR_HIP(hipSetDevice(p->device));
+  return spectral_forward(p, SPEC_LATENT, X, n_rows, params, nullptr, out, (hipStream_t)stream);
+}
+
 extern "C" int tr_forward(tr_plan* p, const float* X, int64_t n_rows, const float* params, const float* weights,
                           float* out, void* stream) {
   if (p == nullptr) return fail(TR_E_ARG, "plan is NULL");
@@ -337,6 +470,7 @@ extern "C" int tr_forward(tr_plan* p, const float* X, int64_t n_rows, const floa
   if (n_rows < 1) return 0;
   hipStream_t st = (hipStream_t)stream;
   TR_HIP(hipSetDevice(p->device));
+  if (p->model == TR_MODEL_SPECTRAL) return spectral_forward(p, SPEC_PRED, X, n_rows, params, weights, out, st);
   int rc = factor_prep(p, params, weights, nullptr, st);
   if (rc) return rc;
   const int mode = p->model == TR_MODEL_LINEAR ? MODE_LIN_PRED : MODE_MNL_PRED;
@@ -365,6 +499,29 @@ extern "C" int tr_loss_grad(tr_plan* p, const float* X, int64_t n_rows, const vo
   if (n_rows == 0) {
     // an empty shard contributes nothing to the all-reduced sum
     TR_HIP(hipMemsetAsync(grad_out, 0, (size_t)p->ngrads * 4, st));
+    return 0;
+  }
+  if (p->model == TR_MODEL_SPECTRAL) {
+    const int reverse = (int)(p->parity & 1u);
+    p->parity++;
+    {
+      TimedLaunch tl(p, st, TR_KERNEL_PREP);
+      TR_HIP(launch_spec_prep(p->sg, params, p->sp_beta, p->sp_thr, p->phi, p->dphi, p->Phi0, stop_flag, st));
+    }
+    const int64_t rpw = (n_rows + p->sgrid - 1) / p->sgrid;
+    {
+      TimedLaunch tl(p, st, TR_KERNEL_STREAM_FUSED);
+      TR_HIP(launch_spec_fused(SPEC_TRAIN, p->sg, p->sgrid, X, n_rows, p->phi, p->Phi0, weights,
+                               (const float*)target, (float)(2.0 / norm), p->gpart, p->slab_stride, p->dpart, yhat_out,
+                               rpw, reverse, stop_flag, st));
+    }
+    {
+      TimedLaunch tl(p, st, TR_KERNEL_REDUCE);
+      TR_HIP(launch_reduce_slabs(4, p->gpart, p->sgrid, p->slab_stride, p->G, p->dpart, p->sgrid, 1.0 / norm,
+                                 grad_out + p->nparams, nullptr, stop_flag, st));
+    }
+    TimedLaunch tl(p, st, TR_KERNEL_MTTKRP);
+    TR_HIP(launch_spec_chain(p->nparams, p->G, p->dphi, grad_out, stop_flag, st));
     return 0;
   }
   int rc = factor_prep(p, params, weights, stop_flag, st);
@@ -482,6 +639,7 @@ extern "C" int tr_adam_step(tr_plan* p, float* params, const float* grad, float*
   ua.iter = iter;
   ua.patience = patience;
   ua.tol = tol;
+  ua.nan_stop = p->model == TR_MODEL_SPECTRAL;  // spectral fit_Adam's NaN stop (spectral…py:738-741)
   TimedLaunch tl(p, (hipStream_t)stream, TR_KERNEL_UPDATE);
   TR_HIP(launch_update(p->fs, p->has_bias, params, grad, ua, exp_avg, exp_avg_sq, max_exp_avg_sq, nullptr, nullptr,
                        loss_hist, stop_flag, (hipStream_t)stream));

@@ -28,6 +28,7 @@ struct UpdateArgs {
   int64_t iter;
   int64_t patience;
   double tol;
+  int nan_stop;        // spectral fit_Adam: stop (not converged) on a NaN loss while iter <= patience
 };
 
 // Launch helpers (all asynchronous on `st`).  Return hipError_t of the launch.
@@ -63,7 +64,7 @@ hipError_t launch_reduce_slabs(int W, const float* part, int64_t nslabs, int64_t
                                float* bias_slot, const int32_t* stop, hipStream_t st);
 hipError_t launch_mttkrp(const FactorSet& fs, const float* phi, const float* dphi, const float* w,
                          const float* G, float* grad, const int32_t* stop, hipStream_t st);
-hipError_t launch_update(const FactorSet& fs, int has_bias, float* params, const float* grad,
+hipError_t launch_update(const FactorSet& fs, int n_bias, float* params, const float* grad,
                          const UpdateArgs& ua, float* m, float* v, float* vmax, float* grad_total_out,
                          float* loss_out, double* loss_hist, int32_t* stop, hipStream_t st);
 

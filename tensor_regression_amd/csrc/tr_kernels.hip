@@ -913,7 +913,7 @@ __device__ double np_pairwise_sum_absdiff(const double* h, int64_t n) {
   return total;
 }
 
-__global__ __launch_bounds__(1024) void k_update(FactorSet fs, int has_bias, float* __restrict__ params,
+__global__ __launch_bounds__(1024) void k_update(FactorSet fs, int n_bias, float* __restrict__ params,
                                                  const float* __restrict__ grad, UpdateArgs ua,
                                                  float* __restrict__ m, float* __restrict__ v,
                                                  float* __restrict__ vmax,
@@ -957,7 +957,7 @@ __global__ __launch_bounds__(1024) void k_update(FactorSet fs, int has_bias, flo
     __syncthreads();
   }
   const int64_t nfe = fs.nfelem;
-  const int64_t np = nfe + (has_bias ? 1 : 0);
+  const int64_t np = nfe + n_bias;  // bias entries after the factors (linear 1, spectral n_out)
   const float lam = ua.lambda_l2;
   for (int64_t e = t; e < np; e += blockDim.x) {
     float g = grad[e];
@@ -994,6 +994,10 @@ __global__ __launch_bounds__(1024) void k_update(FactorSet fs, int has_bias, flo
     const float total = grad[np] + lam * l2;
     if (loss_out != nullptr) *loss_out = total;
     if (ua.mode == 0 && loss_hist != nullptr) loss_hist[ua.hist_base + ua.iter] = (double)total;
+    // spectral…py:738-741: `elif np.isnan(loss_running[-1])` only while ii <= patience;
+    // a negative flag = stopped without convergence, |flag| iterations run
+    if (ua.mode == 0 && ua.nan_stop && stop != nullptr && ua.iter <= ua.patience && __builtin_isnan(total))
+      *stop = -(int32_t)(ua.iter + 1);
   }
 }
 
@@ -1254,10 +1258,10 @@ hipError_t launch_mttkrp(const FactorSet& fs, const float* phi, const float* dph
   return mttkrp_launch_r<64>(fs, phi, dphi, w, G, grad, use_lds, stop, st, grid, lds);
 }
 
-hipError_t launch_update(const FactorSet& fs, int has_bias, float* params, const float* grad,
+hipError_t launch_update(const FactorSet& fs, int n_bias, float* params, const float* grad,
                          const UpdateArgs& ua, float* m, float* v, float* vmax, float* grad_total_out,
                          float* loss_out, double* loss_hist, int32_t* stop, hipStream_t st) {
-  hipLaunchKernelGGL(k_update, dim3(1), dim3(1024), 0, st, fs, has_bias, params, grad, ua, m, v, vmax,
+  hipLaunchKernelGGL(k_update, dim3(1), dim3(1024), 0, st, fs, n_bias, params, grad, ua, m, v, vmax,
                      grad_total_out, loss_out, loss_hist, stop);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;

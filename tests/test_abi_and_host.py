@@ -131,3 +131,39 @@ def test_model_constructors_cpu_only():
     assert mm.n_classes == 4 and [tuple(a.shape) for a in mm.Bcp] == [(5, 2), (3, 2), (4, 2)]
     with pytest.raises(TypeError):
         m.fit_Adam(torch.zeros(10, 6, 4), torch.zeros(10))
+
+
+def test_spectral_plan_validation_without_gpu():
+    from tensor_regression_amd import _lib
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    nn = (ctypes.c_int32 * 3)(0, 0, 0)
+    # rank_normal + rank_spectral == 0, negative dims: argument errors
+    assert lib.tr_plan_create_spectral(ctypes.byref(h), 0, 8, 5, 2, 0, 0, 2, 10, nn, 50.0, 1.0) == -1
+    assert lib.tr_plan_create_spectral(ctypes.byref(h), 0, 0, 5, 2, 1, 1, 2, 10, nn, 50.0, 1.0) == -1
+    # outside the kernel envelope: K > 32, W > 256, one sample beyond LDS
+    assert lib.tr_plan_create_spectral(ctypes.byref(h), 0, 8, 5, 2, 8, 13, 2, 10, nn, 50.0, 1.0) == -2
+    assert lib.tr_plan_create_spectral(ctypes.byref(h), 0, 300, 5, 2, 2, 2, 2, 10, nn, 50.0, 1.0) == -2
+    assert lib.tr_plan_create_spectral(ctypes.byref(h), 0, 256, 256, 2, 2, 2, 2, 10, nn, 50.0, 1.0) == -2
+    assert b"LDS" in lib.tr_last_error()
+
+
+@pytest.mark.parametrize("name", ["spec_basic", "spec_nonneg_amsgrad_wd", "spec_cc1_softplus", "spec_rn0"])
+def test_spectral_constructor_matches_reference_init(name):
+    """CP_linear_regression.__init__ (spectral…py:425-539) draws the same factors for the same seed."""
+    import json
+    import torch
+    from tensor_regression_amd.spectral_tensor_regression import CP_linear_regression
+    d = dict(np.load(os.path.join(ROOT, "tests", "golden", name + ".npz")))
+    m = json.loads(str(d["meta"]))
+    torch.manual_seed(m["seed"])
+    X_shape = (len(d["y"]),) + tuple(m["shape"][1:])
+    model = CP_linear_regression(X_shape, (len(d["y"]), m["n_out"]), rank_normal=m["rank_normal"],
+                                 rank_spectral=m["rank_spectral"], non_negative=m["non_negative"],
+                                 n_complex_dim=m["n_complex_dim"], softplus_kwargs=m["softplus_kwargs"])
+    got_n = np.concatenate([a.detach().numpy().reshape(-1) for a in model.Bcp_n])
+    got_c = np.concatenate([a.detach().numpy().reshape(-1) for a in model.Bcp_c])
+    np.testing.assert_array_equal(got_n, d["Bcp_n0"])
+    np.testing.assert_array_equal(got_c, d["Bcp_c0"])
+    assert [tuple(a.shape) for a in model.Bcp_c] == [tuple(s) for s in m["factor_shapes_c"]]
+    assert model.bias.shape == (m["n_out"],) and all(a.requires_grad for a in model.Bcp_n + model.Bcp_c)
