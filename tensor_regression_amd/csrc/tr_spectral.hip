@@ -159,7 +159,7 @@ __global__ __launch_bounds__(kSpecT) void k_spec_fused(
   constexpr int KP = 16 * KT;       // padded K
   constexpr int NGRP = NW / KT;     // wave groups over d tiles (= w tiles per row block)
   constexpr int TPW = KT;           // d tiles per wave per set (NGRP * TPW = 8 tiles per set)
-  constexpr int RB = 16 * NGRP;     // rows per block (64 or 128)
+  constexpr int RB = 128;           // rows per LDS-DMA / gradient block
   constexpr int PHS = RB / 4;       // forward k steps per block
   constexpr int NBMAX = 256 / RB;   // row blocks at W = 256
   constexpr int NPH = WSMAX / PHS;  // forward phases the step bound allows
@@ -178,8 +178,9 @@ __global__ __launch_bounds__(kSpecT) void k_spec_fused(
   float* sT = lds + g.oT;
   float* sTail = lds + g.oTail;    // [NGRP][Dtail][KP] partial-tile partials
   float* sZV = lds + g.oSm;        // [64]  Z (Rn) | V (Rs)     or  Z | U (K) in predict mode
-  float* sDZV = sZV + 64;          // [64]  dZ (Rn) | dV (Rs)
-  float* sY = sDZV + 64;           // [NO]  y of the current sample
+  float* sDZ = sZV + 32;           // [32]  dZ (Rn) | dV (Rs)   (the fit mode reduces <= 32 values)
+  float* sRv = sZV + 64;           // [NO]  residual * MSE scale (NO <= 256 fits with sY after it)
+  float* sY = sRv + 256;           // [NO]  y of the current sample
   float* sAcc = lds + g.oAcc;      // [NO*Rn] dA2 | [NO*Rs] dC2 | [NO] dbias
   float* sPA1 = lds + g.oPhi;      // [Rn][D]  phi(A1), transposed: consecutive d -> consecutive banks
   float* sPC1 = sPA1 + D * Rn;     // [Rs][D]  phi(C1), transposed
@@ -213,13 +214,16 @@ __global__ __launch_bounds__(kSpecT) void k_spec_fused(
       bf[s] = (w < g.W && col < K) ? Phi0[(int64_t)w * K + col] : 0.f;
     }
   }
-  // gradient tiles: w tile NGRP*p + grp, column tile ktw; two accumulators (even / odd k steps)
-  tr_f32x4_s gacc[NBMAX][2];
+  // gradient tiles: w tiles 8p + grp + NGRP*u (u < KT) of block p, column tile ktw; two
+  // accumulators each (even / odd k steps)
+  tr_f32x4_s gacc[NBMAX][KT][2];
 #pragma unroll
-  for (int p = 0; p < NBMAX; ++p) {
-    gacc[p][0] = tr_f32x4_s{0.f, 0.f, 0.f, 0.f};
-    gacc[p][1] = tr_f32x4_s{0.f, 0.f, 0.f, 0.f};
-  }
+  for (int p = 0; p < NBMAX; ++p)
+#pragma unroll
+    for (int u = 0; u < KT; ++u) {
+      gacc[p][u][0] = tr_f32x4_s{0.f, 0.f, 0.f, 0.f};
+      gacc[p][u][1] = tr_f32x4_s{0.f, 0.f, 0.f, 0.f};
+    }
   float* sl = slab != nullptr ? slab + (int64_t)blockIdx.x * slab_stride : nullptr;
   // gradients of A1 / C1 in phi space, item e = j*D + d (j < Rn: A1[d, j]; else C1[d, j - Rn]),
   // thread t owns items t + 512*m (D*(Rn+Rs) <= 256*32 = 512*16)
@@ -272,6 +276,10 @@ __global__ __launch_bounds__(kSpecT) void k_spec_fused(
     }
     return cnt;
   };
+#if TR_SPEC_PROFILE
+  unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long prof_t = 0;
+#endif
   int cnt_blk[NBMAX];  // this wave's DMA instructions per block of the sample in flight
 #pragma unroll
   for (int p = 0; p < NBMAX; ++p) cnt_blk[p] = 0;
@@ -286,8 +294,14 @@ __global__ __launch_bounds__(kSpecT) void k_spec_fused(
 #pragma unroll
     for (int q = 0; q < NBMAX; ++q)
       if (q > p && q < NB) later += cnt_blk[q];
+#if TR_SPEC_PROFILE
+    const unsigned long long w0 = __builtin_readcyclecounter();
+#endif
     spec_wait_vm(later);
     spec_barrier();
+#if TR_SPEC_PROFILE
+    prof[5] += __builtin_readcyclecounter() - w0;
+#endif
   };
 
   // y of the next sample is prefetched into a register one iteration ahead (thread o = t < NO)
@@ -295,8 +309,7 @@ __global__ __launch_bounds__(kSpecT) void k_spec_fused(
   if (nr > 0 && !(TR_SPEC_SKIP & 8)) issue_all(sample_of(0));
 
 #if TR_SPEC_PROFILE
-  unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  unsigned long long prof_t = __builtin_readcyclecounter();
+  prof_t = __builtin_readcyclecounter();
 #endif
 #pragma unroll 1
   for (int64_t k = 0; k < nr; ++k) {
@@ -392,44 +405,74 @@ __global__ __launch_bounds__(kSpecT) void k_spec_fused(
     if (MODE == SPEC_TRAIN && t < NO) sY[t] = ycur;
     spec_barrier();
     if (MODE != SPEC_TRAIN && has_next) issue_all(sample_of(k + 1));  // X_n is no longer read
+    if (g.Dtail > 0) {  // partial d tile: sum the wave groups' partials into T
+      const int d16 = 16 * g.nDF;
+      for (int e = t; e < g.Dtail * K; e += kSpecT) {
+        const int row = e / K, col = e - row * K;
+        float v = sTail[row * KP + col];
+#pragma unroll
+        for (int gg = 1; gg < NGRP; ++gg) v += sTail[(gg * g.Dtail + row) * KP + col];
+        sT[(d16 + row) * KS + col] = v;
+      }
+      spec_barrier();
+    }
     TR_PROF_MARK(0);
 
     // ---- epilogue: column sums over d (Z, V or U) by groups of TPV lanes --------------------
     // value j is summed by lanes [j*TPV, (j+1)*TPV) over rows d = q, q + TPV, ... and reduced
-    // with a fixed xor butterfly inside the group (deterministic); rows of the partial d tile
-    // are summed from the wave groups' partials and written back into T here
+    // with a fixed xor butterfly inside the group (deterministic)
     const int nred = (TR_SPEC_SKIP & 2) ? 0 : (MODE == SPEC_TRAIN ? Rn + Rs : (MODE == SPEC_PRED ? K : Rn));
     {
       const int TPV = nred <= 16 ? 32 : 16;
       const int j = t / TPV, q = t - j * TPV;
-      const int d16 = 16 * g.nDF;
-      auto tval = [&](int d, int col) -> float {  // T[d][col], materialising partial-tile rows
-        if (d < d16) return sT[d * KS + col];
-        const int row = d - d16;
-        float v = sTail[row * KP + col];
-        for (int gg = 1; gg < NGRP; ++gg) v += sTail[(gg * g.Dtail + row) * KP + col];
-        sT[d * KS + col] = v;
-        return v;
-      };
+      auto tval = [&](int d, int col) -> float { return sT[d * KS + col]; };
       float v = 0.f;
       if (j < nred) {
-        if (j < Rn) {
-          const float* ph = sPA1 + j * D;
-          for (int d = q; d < D; d += TPV) v = fmaf(tval(d, j), ph[d], v);
-        } else if (MODE == SPEC_TRAIN) {
+        // rows d = q + TPV*m, m < 16 (D <= 256): unrolled so that every LDS read is in flight at once
+        if (j < Rn || MODE != SPEC_TRAIN) {
+          const float* ph = (j < Rn ? sPA1 + j * D : sPC1 + ((j - Rn) / Cc) * D);
+          for (int m0 = 0; m0 < 16 && q + TPV * m0 < D; m0 += 8) {
+            float tv[8], pv[8];
+#pragma unroll
+            for (int m = 0; m < 8; ++m) {
+              const int d = q + TPV * (m0 + m);
+              tv[m] = d < D ? tval(d, j) : 0.f;
+              pv[m] = d < D ? ph[d] : 0.f;
+            }
+#pragma unroll
+            for (int m = 0; m < 8; ++m) v = fmaf(tv[m], pv[m], v);
+          }
+        } else {
           const int r = j - Rn;
           const float* ph = sPC1 + r * D;
-          for (int d = q; d < D; d += TPV) {
-            float ss = 0.f;
-            for (int c = 0; c < Cc; ++c) {
-              const float x = tval(d, Rn + r * Cc + c);
-              ss = fmaf(x, x, ss);
+          const int c0 = Rn + r * Cc;
+          for (int m0 = 0; m0 < 16 && q + TPV * m0 < D; m0 += 8) {
+          float ss[8], pv[8];
+#pragma unroll
+          for (int m = 0; m < 8; ++m) {
+            const int d = q + TPV * (m0 + m);
+            float acc2 = 0.f;
+            if (d < D) {
+              if (Cc <= 4) {
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                  if (c < Cc) {
+                    const float x = tval(d, c0 + c);
+                    acc2 = fmaf(x, x, acc2);
+                  }
+              } else {
+                for (int c = 0; c < Cc; ++c) {
+                  const float x = tval(d, c0 + c);
+                  acc2 = fmaf(x, x, acc2);
+                }
+              }
             }
-            v = fmaf(sqrtf(ss), ph[d], v);
+            ss[m] = acc2;
+            pv[m] = d < D ? ph[d] : 0.f;
           }
-        } else {  // predict: U[r, c] = sum_d phi(C1)[d, r] T[d, Rn + r*Cc + c]
-          const float* ph = sPC1 + ((j - Rn) / Cc) * D;
-          for (int d = q; d < D; d += TPV) v = fmaf(tval(d, j), ph[d], v);
+#pragma unroll
+          for (int m = 0; m < 8; ++m) v = fmaf(sqrtf(ss[m]), pv[m], v);
+          }
         }
       }
       if (TPV == 32) v += tr_swz_xor<0x401F>(v);  // xor 16
@@ -469,42 +512,84 @@ __global__ __launch_bounds__(kSpecT) void k_spec_fused(
       continue;
     }
 
-    // ---- SPEC_TRAIN: y_hat, residual, loss and the small-factor gradients in one step: each of
-    // the Rn + Rs threads recomputes the NO residuals it needs (no barrier in between)
-    if (t < Rn + Rs) {
+    // ---- SPEC_TRAIN: y_hat, residual, loss and the small-factor gradients --------------------
+    // lane (o, r) = (t / 32, t % 32) holds coefficient r of output o; y_hat_o by a 32-lane xor
+    // butterfly; the residual (times the MSE scale) goes to sRv for the dT step
+    {
+      const int KR = Rn + Rs;
       const float bm = (float)((Rn > 0) + (Rs > 0));  // the bias is added by both terms (Q10)
-      float dz = 0.f;
-      const float zt = sZV[t];
-      const float wt_ = t < Rn ? sWt[t] : 1.f;
-      for (int o = 0; o < NO; ++o) {
-        const float b = sB[o];
-        float yh = 0.f;
-        if (Rn > 0) {
-          float yl = 0.f;
+      if (NO <= kSpecT / 32) {
+        const int o = t >> 5, r = t & 31;
+        const bool act = o < NO && r < KR;
+        float c = 0.f, zr = 0.f;
+        if (act) {
+          c = r < Rn ? sPA2[o * Rn + r] : sPC2[o * Rs + (r - Rn)];
+          zr = sZV[r];
+        }
+        float pl = r < Rn ? c * zr : 0.f;
+        float ps = r < Rn ? 0.f : c * zr;
+        pl += tr_swz_xor<0x401F>(pl);
+        ps += tr_swz_xor<0x401F>(ps);
+        pl += tr_swz_xor<0x201F>(pl);
+        ps += tr_swz_xor<0x201F>(ps);
+        pl += tr_swz_xor<0x101F>(pl);
+        ps += tr_swz_xor<0x101F>(ps);
+        pl += tr_swz_xor<0x081F>(pl);
+        ps += tr_swz_xor<0x081F>(ps);
+        pl += tr_swz_xor<0x041F>(pl);
+        ps += tr_swz_xor<0x041F>(ps);
+        if (o < NO) {
+          const float b = sB[o];
+          const float yh = (Rn > 0 ? pl + b : 0.f) + (Rs > 0 ? ps + b : 0.f);
+          const float e = yh - sY[o];
+          const float rv = e * scale;
+          if (act) {
+            if (r < Rn)
+              sAcc[o * Rn + r] += sWt[r] * rv * zr;
+            else
+              sAcc[NO * Rn + o * Rs + (r - Rn)] += rv * zr;
+          }
+          if (r == 0) {
+            sRv[o] = rv;
+            sAcc[NO * KR + o] += bm * rv;
+            lsum += (double)e * (double)e;
+            if (out != nullptr) out[n * NO + o] = yh;
+          }
+        }
+      } else {  // many outputs: one thread per output, then one per coefficient
+        for (int o = t; o < NO; o += kSpecT) {
+          const float b = sB[o];
+          float yl = 0.f, ys = 0.f;
           for (int r = 0; r < Rn; ++r) yl = fmaf(sPA2[o * Rn + r], sZV[r], yl);
-          yh = yl + b;
-        }
-        if (Rs > 0) {
-          float ys = 0.f;
           for (int r = 0; r < Rs; ++r) ys = fmaf(sPC2[o * Rs + r], sZV[Rn + r], ys);
-          yh = yh + (ys + b);
-        }
-        const float e = yh - sY[o];
-        const float rv = e * scale;
-        if (t < Rn) {
-          dz = fmaf(rv, sPA2[o * Rn + t], dz);  // sPA2 holds w_r * phi(A2)
-          sAcc[o * Rn + t] += wt_ * rv * zt;
-        } else {
-          dz = fmaf(rv, sPC2[o * Rs + (t - Rn)], dz);
-          sAcc[NO * Rn + o * Rs + (t - Rn)] += rv * zt;
-        }
-        if (t == 0) {
-          if (out != nullptr) out[n * NO + o] = yh;
+          const float yh = (Rn > 0 ? yl + b : 0.f) + (Rs > 0 ? ys + b : 0.f);
+          const float e = yh - sY[o];
+          const float rv = e * scale;
+          sRv[o] = rv;
+          sAcc[NO * KR + o] += bm * rv;
           lsum += (double)e * (double)e;
-          sAcc[NO * (Rn + Rs) + o] += bm * rv;
+          if (out != nullptr) out[n * NO + o] = yh;
+        }
+        spec_barrier();
+        for (int e2 = t; e2 < NO * KR; e2 += kSpecT) {
+          const int o = e2 / KR, r = e2 - o * KR;
+          const float rv = sRv[o];
+          if (r < Rn)
+            sAcc[o * Rn + r] += sWt[r] * rv * sZV[r];
+          else
+            sAcc[NO * Rn + o * Rs + (r - Rn)] += rv * sZV[r];
         }
       }
-      sDZV[t] = dz;
+    }
+    spec_barrier();
+    // dZ_j / dV_j = sum_o residual_o * coefficient(o, j)  (one thread per coefficient column)
+    if (t < Rn + Rs) {
+      float dz = 0.f;
+      if (t < Rn)
+        for (int o = 0; o < NO; ++o) dz = fmaf(sRv[o], sPA2[o * Rn + t], dz);  // sPA2 = w_r phi(A2)
+      else
+        for (int o = 0; o < NO; ++o) dz = fmaf(sRv[o], sPC2[o * Rs + (t - Rn)], dz);
+      sDZ[t] = dz;
     }
     spec_barrier();
     TR_PROF_MARK(2);
@@ -516,20 +601,37 @@ __global__ __launch_bounds__(kSpecT) void k_spec_fused(
         int j, d;
         item(e, j, d);
         float* Tw = sT + d * KS;
-        const float dz = sDZV[j];
+        const float dz = sDZ[j];
         if (j < Rn) {
           const float tv = Tw[j];
+          const float ph = sPA1[j * D + d];
           acc[m] = fmaf(dz, tv, acc[m]);
-          Tw[j] = dz * sPA1[j * D + d];
+          Tw[j] = dz * ph;
         } else {
           const int r = j - Rn;
           float* tp = Tw + Rn + r * Cc;
-          float ss = 0.f;
-          for (int c = 0; c < Cc; ++c) ss = fmaf(tp[c], tp[c], ss);
-          const float mg = sqrtf(ss);
-          acc[m] = fmaf(dz, mg, acc[m]);
-          const float qq = mg > 0.f ? dz * sPC1[r * D + d] / mg : 0.f;
-          for (int c = 0; c < Cc; ++c) tp[c] *= qq;
+          const float ph = sPC1[r * D + d];
+          if (Cc <= 4) {
+            float xv[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) xv[c] = c < Cc ? tp[c] : 0.f;
+            float ss = 0.f;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) ss = fmaf(xv[c], xv[c], ss);
+            const float mg = sqrtf(ss);
+            acc[m] = fmaf(dz, mg, acc[m]);
+            const float qq = mg > 0.f ? dz * ph * __builtin_amdgcn_rcpf(mg) : 0.f;
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+              if (c < Cc) tp[c] = qq * xv[c];
+          } else {
+            float ss = 0.f;
+            for (int c = 0; c < Cc; ++c) ss = fmaf(tp[c], tp[c], ss);
+            const float mg = sqrtf(ss);
+            acc[m] = fmaf(dz, mg, acc[m]);
+            const float qq = mg > 0.f ? dz * ph * __builtin_amdgcn_rcpf(mg) : 0.f;
+            for (int c = 0; c < Cc; ++c) tp[c] *= qq;
+          }
         }
       }
     }
@@ -539,33 +641,40 @@ __global__ __launch_bounds__(kSpecT) void k_spec_fused(
     TR_PROF_MARK(3);
 
     // ---- gradient GEMM by row blocks: dPhi0[w, k] += sum_d X_n[w, d] dT_n[d, k] ----------------
-    // wave = (w tile NGRP*p + grp, column tile ktw); step s covers d = 64*(s/16) + 16*j + s%16
-    // (conflict-free A and B reads; rows d >= D read the zero row D of dT); 4-step chunks, the
-    // next chunk's loads issued right behind the current chunk's MFMAs
+    // wave = (w tiles 8p + grp + NGRP*u, column tile ktw); step s covers d = 64*(s/16) + 16*j +
+    // s%16 (conflict-free A and B reads; rows d >= D read the zero row D of dT); 4-step chunks,
+    // the next chunk's loads issued right behind the current chunk's MFMAs
     const int nch = (g.DS + 3) >> 2;
 #pragma unroll
     for (int p = 0; p < NBMAX; ++p) {
       if (p < NB) {
-        const int wt = NGRP * p + grp;
-        if (wt < g.nWT && !(TR_SPEC_SKIP & 4)) {
-          const float* xw = sX + (wt * 16 + i) * S + 16 * gq;
+        if (!(TR_SPEC_SKIP & 4)) {
+          const float* xw[KT];
+          bool wok[KT];
+#pragma unroll
+          for (int u = 0; u < KT; ++u) {
+            const int wt = 8 * p + grp + NGRP * u;
+            wok[u] = wt < g.nWT;
+            xw[u] = sX + ((wok[u] ? wt : 0) * 16 + i) * S + 16 * gq;
+          }
           const float* tb = sT + ktw * 16 + i;
-          float xA[4], xB[4], bA[4], bB[4];
-          auto ld = [&](float(&xx)[4], float(&bb)[4], int c) {
+          float xA[KT][4], xB[KT][4], bA[4], bB[4];
+          auto ld = [&](float(&xx)[KT][4], float(&bb)[4], int c) {
 #pragma unroll
             for (int v = 0; v < 4; ++v) {
               const int st = 4 * c + v;
               const int d0 = 64 * (st >> 4) + (st & 15);
               const int d = d0 + 16 * gq;
-              xx[v] = xw[d0];
+#pragma unroll
+              for (int u = 0; u < KT; ++u) xx[u][v] = xw[u][d0];
               bb[v] = tb[(d < D ? d : D) * KS];
             }
           };
-          auto mm = [&](const float(&xx)[4], const float(&bb)[4]) {
-            gacc[p][0] = mfma4(xx[0], bb[0], gacc[p][0]);
-            gacc[p][1] = mfma4(xx[1], bb[1], gacc[p][1]);
-            gacc[p][0] = mfma4(xx[2], bb[2], gacc[p][0]);
-            gacc[p][1] = mfma4(xx[3], bb[3], gacc[p][1]);
+          auto mm = [&](const float(&xx)[KT][4], const float(&bb)[4]) {
+#pragma unroll
+            for (int v = 0; v < 4; ++v)
+#pragma unroll
+              for (int u = 0; u < KT; ++u) gacc[p][u][v & 1] = mfma4(xx[u][v], bb[v], gacc[p][u][v & 1]);
           };
           ld(xA, bA, 0);
           for (int c = 0; c < nch; c += 2) {
@@ -578,8 +687,14 @@ __global__ __launch_bounds__(kSpecT) void k_spec_fused(
           }
         }
         if (has_next) {
+#if TR_SPEC_PROFILE
+          const unsigned long long w0 = __builtin_readcyclecounter();
+#endif
           spec_barrier();  // every wave's reads of rows [RB*p, RB*(p+1)) have retired
           cnt_blk[p] = issue(sample_of(k + 1), p);
+#if TR_SPEC_PROFILE
+          prof[6] += __builtin_readcyclecounter() - w0;
+#endif
         }
       }
     }
@@ -596,17 +711,20 @@ __global__ __launch_bounds__(kSpecT) void k_spec_fused(
   {
     const int i = lane & 15, gq = lane >> 4;
 #pragma unroll
-    for (int p = 0; p < NBMAX; ++p) {
-      const int wt = NGRP * p + grp;
+    for (int p = 0; p < NBMAX; ++p)
 #pragma unroll
-      for (int reg = 0; reg < 4; ++reg) {
-        const int w = wt * 16 + 4 * gq + reg, kk = ktw * 16 + i;
-        if (p < NB && wt < g.nWT && w < g.W && kk < K) {
-          const int64_t dst = kk < Rn ? g.offA0 + (int64_t)w * Rn + kk : g.offC0 + (int64_t)w * Rs * Cc + (kk - Rn);
-          sl[dst] = gacc[p][0][reg] + gacc[p][1][reg];
+      for (int u = 0; u < KT; ++u) {
+        const int wt = 8 * p + grp + NGRP * u;
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {
+          const int w = wt * 16 + 4 * gq + reg, kk = ktw * 16 + i;
+          if (p < NB && wt < g.nWT && w < g.W && kk < K) {
+            const int64_t dst =
+                kk < Rn ? g.offA0 + (int64_t)w * Rn + kk : g.offC0 + (int64_t)w * Rs * Cc + (kk - Rn);
+            sl[dst] = gacc[p][u][0][reg] + gacc[p][u][1][reg];
+          }
         }
       }
-    }
   }
 #pragma unroll
   for (int m = 0; m < AMAX; ++m) {
@@ -623,10 +741,19 @@ __global__ __launch_bounds__(kSpecT) void k_spec_fused(
   for (int e = t; e < NO * Rn; e += kSpecT) sl[g.offA2 + e] = sAcc[e];
   for (int e = t; e < NO * Rs; e += kSpecT) sl[g.offC2 + e] = sAcc[NO * Rn + e];
   for (int e = t; e < NO; e += kSpecT) sl[g.offB + e] = sAcc[NO * (Rn + Rs) + e];
-  // data loss partial: only thread 0 accumulated it
-  if (t == 0) {
-    dpart[2 * blockIdx.x] = lsum;
-    dpart[2 * blockIdx.x + 1] = 0.0;
+  // data loss partial: fixed-order block reduction (each output's thread accumulated its own)
+  {
+    double* dred = reinterpret_cast<double*>(lds + g.oRed);
+    const double ls = tr_wave_allreduce_d(lsum);
+    __syncthreads();
+    if (lane == 0) dred[wv] = ls;
+    __syncthreads();
+    if (t == 0) {
+      double tot = 0.0;
+      for (int w = 0; w < NW; ++w) tot += dred[w];
+      dpart[2 * blockIdx.x] = tot;
+      dpart[2 * blockIdx.x + 1] = 0.0;
+    }
   }
 }
 
@@ -671,8 +798,7 @@ bool spec_geom_init(SpecGeom* g, int64_t W, int64_t D, int64_t NO, int Rn, int R
   g->S = (int)D;  // lane-linear LDS image of the sample (LDS-DMA); odd D => conflict-free MFMA reads
   g->KS = 16 * g->KT + 1;
   g->nWT = cdiv_i(W, 16);
-  const int RB = g->KT == 2 ? 64 : 128;  // row block of the LDS-DMA / gradient GEMM (16 * 8/KT rows)
-  g->Wrows = RB * cdiv_i(W, RB);         // zero-padded rows: the forward walks whole row blocks
+  g->Wrows = 128 * cdiv_i(W, 128);  // zero-padded rows: the forward walks whole 128-row blocks
   g->nDF = (int)(D / 16);
   g->Dtail = (int)(D % 16);
   g->WS = g->Wrows / 4;  // forward k steps over the zero-padded row blocks
@@ -701,7 +827,7 @@ bool spec_geom_init(SpecGeom* g, int64_t W, int64_t D, int64_t NO, int Rn, int R
   const int TF = round4((int64_t)(D + 1) * g->KS);  // + one zero row (the gradient GEMM's pad rows)
   const int TailF = kSpecNW * g->Dtail * 16 * g->KT;
   const int RedF = 64;  // loss reduction (one double per wave)
-  const int SmF = round4(128 + NO);  // Z/V, dZ/dV, y
+  const int SmF = round4(64 + 256 + NO);  // Z/V (or U), residuals, y
   const int AccF = round4(NO * (int64_t)(Rn + Rs + 1));
   g->oT = XF;
   g->oTail = g->oT + TF;

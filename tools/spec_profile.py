@@ -4,12 +4,9 @@
     make -C tensor_regression_amd/csrc prof
     TR_HIP_LIB=$PWD/tensor_regression_amd/libtr_hip_prof.so python tools/spec_profile.py
 
-Phases (wave 0 of each workgroup, s_memtime-free __builtin_readcyclecounter deltas):
-  0 loop top -> forward GEMM of the full d tiles done (includes the LDS-DMA waits)
-  1 partial-tile forward + tail reduction
-  2 column-sum epilogue (Z, V)
-  3 y_hat / residual / small grads / dT
-  4 gradient GEMM + next-sample DMA issue
+Phases (wave 0 of each workgroup, __builtin_readcyclecounter deltas): forward GEMM (with the
+LDS-DMA waits), column sums, y_hat/residual/small-factor grads, dT + A1/C1 grads, gradient GEMM
+(with the per-block barrier + next-sample DMA issue); two sub-totals split out the waits.
 """
 import ctypes
 import os
@@ -37,10 +34,12 @@ buf = (ctypes.c_ulonglong * (256 * 8))()
 assert fn(buf) == 0
 rows = [[buf[b * 8 + q] for q in range(8)] for b in range(256)]
 per_wg = N // 256
-names = ["fwd full tiles (+DMA waits)", "partial tile + tail sum", "column sums", "yhat/resid/dT", "grad GEMM + DMA issue"]
+names = ["fwd GEMM (+DMA waits)", "column sums", "yhat/resid/small grads", "dT + A1/C1 grads", "grad GEMM + DMA issue",
+         "  of which DMA waits (fwd)", "  of which barrier+DMA issue (grad)"]
 tot = 0
 for q, nm in enumerate(names):
     avg = sum(r[q] for r in rows) / 256 / per_wg
-    tot += avg
-    print(f"{nm:32s} {avg:10.0f} cycles/sample")
+    if q < 5:
+        tot += avg
+    print(f"{nm:36s} {avg:10.0f} cycles/sample")
 print(f"{'total':32s} {tot:10.0f} cycles/sample  (x {per_wg} samples/WG)")
