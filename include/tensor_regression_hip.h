@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define TR_ABI_VERSION 2
+#define TR_ABI_VERSION 3
 
 #define TR_MODEL_LINEAR 0      /* CP_linear_regression: y_hat = <X, [[w; Phi]]> + bias, MSE */
 #define TR_MODEL_MULTINOMIAL 1 /* CP_logistic_regression: softmax(<X, [[w; Phi]]>), CE(weight) */
@@ -93,6 +93,17 @@ int64_t tr_plan_factor_offset(const tr_plan* plan, int factor);
 int64_t tr_plan_workspace_bytes(const tr_plan* plan);
 /* Human-readable description of the kernel strategy chosen for this plan (host string). */
 const char* tr_plan_describe(const tr_plan* plan);
+
+/*
+ * Row stride of X for the following tr_forward / tr_loss_grad / tr_spectral_latents calls:
+ * sample n starts at X + n*stride floats and its P floats are contiguous (stride 0 = P, the
+ * dense default).  A stride < P expresses the reference's windowed samples
+ * (util.py:67-114, WindowedDataset: sample n = rows [n + w0, n + w1) of an untiled (T, F...)
+ * series) without materialising them: stride = F, P = window * F.  The vector (16-byte) kernel
+ * paths need stride % 4 == 0 and a 16-byte aligned X; otherwise the plan switches to its scalar
+ * paths, and a misaligned X on a vector plan is rejected with TR_E_ARG.
+ */
+int tr_plan_set_x_stride(tr_plan* plan, int64_t stride);
 
 /*
  * Forward model only (predict path).

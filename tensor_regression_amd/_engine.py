@@ -175,17 +175,28 @@ class Plan:
         return {k: (ms[i], cnt[i]) for i, k in enumerate(_lib.KERNEL_KINDS)}
 
     # ---- entry points ------------------------------------------------------------------------
+    def _set_stride(self, X):
+        """Tell the plan X's row stride (windowed / strided views) when it changes."""
+        stride = int(X.stride(0)) if X.ndim >= 1 and X.shape[0] > 1 else 0
+        if stride == int(np.prod(X.shape[1:])):
+            stride = 0
+        if stride != getattr(self, "_xstride", 0):
+            check(self.lib.tr_plan_set_x_stride(self.h, stride), "tr_plan_set_x_stride")
+            self._xstride = stride
+
     def forward(self, X, arena, weights, out=None):
         N = X.shape[0]
         C = self.n_classes if self.model == _lib.TR_MODEL_MULTINOMIAL else 1
         if out is None:
             shape = (N, C) if self.model == _lib.TR_MODEL_MULTINOMIAL else (N,)
             out = torch.empty(shape, dtype=torch.float32, device=X.device)
+        self._set_stride(X)
         rc = self.lib.tr_forward(self.h, ptr(X), N, ptr(arena), ptr(weights), ptr(out), stream_handle(self.dev))
         check(rc, "tr_forward")
         return out
 
     def loss_grad(self, X, target, class_weight, norm, arena, weights, grad, yhat=None, stop=None):
+        self._set_stride(X)
         rc = self.lib.tr_loss_grad(self.h, ptr(X), X.shape[0], ptr(target), ptr(class_weight), float(norm),
                                    ptr(arena), ptr(weights), ptr(grad), ptr(yhat), ptr(stop),
                                    stream_handle(self.dev))
@@ -264,6 +275,7 @@ class SpectralPlan(Plan):
         """The reference's predict model: lin_model + spectral_model (N, n_out)."""
         if out is None:
             out = torch.empty((X.shape[0], self.dims[2]), dtype=torch.float32, device=X.device)
+        self._set_stride(X)
         rc = self.lib.tr_forward(self.h, ptr(X), X.shape[0], ptr(arena), ptr(weights), ptr(out),
                                  stream_handle(self.dev))
         check(rc, "tr_forward")
@@ -273,9 +285,35 @@ class SpectralPlan(Plan):
         """stepwise_latents_model (N, rank_normal)."""
         if out is None:
             out = torch.zeros((X.shape[0], self.rank_normal), dtype=torch.float32, device=X.device)
+        self._set_stride(X)
         rc = self.lib.tr_spectral_latents(self.h, ptr(X), X.shape[0], ptr(arena), ptr(out), stream_handle(self.dev))
         check(rc, "tr_spectral_latents")
         return out
+
+
+def _rows_contiguous(X):
+    """Each X[n] block is contiguous (any stride, even overlapping, along dim 0)."""
+    expect = 1
+    for d in range(X.ndim - 1, 0, -1):
+        if X.shape[d] != 1 and X.stride(d) != expect:
+            return False
+        expect *= X.shape[d]
+    return X.ndim >= 1 and X.stride(0) >= 1
+
+
+def as_device_rows(X, dev):
+    """X as an fp32 tensor on cuda:dev whose samples X[n] are contiguous blocks; the stride along
+    dim 0 is kept (strided / windowed views, e.g. util.windowed_view, are NOT materialised).  A
+    view the 16-byte kernel paths cannot read (misaligned base with a stride % 4 == 0) is copied."""
+    if not isinstance(X, torch.Tensor):
+        X = torch.as_tensor(np.asarray(X), dtype=torch.float32)
+    if X.dtype != torch.float32:
+        raise TypeError(f"the gfx950 path computes in fp32; got X of dtype {X.dtype}")
+    if X.device.type != "cuda" or X.device.index != dev:
+        X = X.to(f"cuda:{dev}")
+    if not _rows_contiguous(X) or (X.stride(0) % 4 == 0 and X.data_ptr() % 16 != 0):
+        X = X.contiguous()
+    return X
 
 
 def as_device_f32(X, dev):
@@ -287,6 +325,23 @@ def as_device_f32(X, dev):
     if X.device.type != "cuda" or X.device.index != dev:
         X = X.to(f"cuda:{dev}")
     return X.contiguous()
+
+
+def loss_grad_any(plan, X, target, class_weight, norm, arena, weights, grad, stop=None, tmp=None):
+    """plan.loss_grad over a device X, or over a util.HostStream chunk by chunk (the chunk arenas
+    are summed like sample shards: every data gradient is already normalised by `norm`)."""
+    from .util import HostStream
+    if not isinstance(X, HostStream):
+        plan.loss_grad(X, target, class_weight, norm, arena, weights, grad, stop=stop)
+        return
+    first = True
+    for r0, r1, Xc in X.chunks():
+        if first:
+            plan.loss_grad(Xc, target[r0:r1], class_weight, norm, arena, weights, grad, stop=stop)
+            first = False
+        else:
+            plan.loss_grad(Xc, target[r0:r1], class_weight, norm, arena, weights, tmp, stop=stop)
+            grad.add_(tmp)
 
 
 def run_adam_fit(plan, X, target, class_weight, norm, arena, weights, lambda_L2, max_iter, tol, patience,
@@ -308,6 +363,7 @@ def run_adam_fit(plan, X, target, class_weight, norm, arena, weights, lambda_L2,
     if base:
         hist[:base] = torch.tensor(loss_running, dtype=torch.float64)
     stop = torch.zeros(1, dtype=torch.int32, device=dev)
+    tmp = torch.zeros_like(grad)
     ii = 0
     stopped_at = 0
     if verbose_cb is not None:
@@ -318,7 +374,7 @@ def run_adam_fit(plan, X, target, class_weight, norm, arena, weights, lambda_L2,
             it = ii + k
             if verbose_cb is not None:
                 verbose_cb.before_step(arena)
-            plan.loss_grad(X, target, class_weight, norm, arena, weights, grad, stop=stop)
+            loss_grad_any(plan, X, target, class_weight, norm, arena, weights, grad, stop=stop, tmp=tmp)
             if allreduce is not None:
                 allreduce(grad)
             plan.adam_step(arena, grad, m, v, vmax, lambda_L2, hp, it + 1, hist, base, it, patience, tol, stop)

@@ -29,6 +29,7 @@ struct tr_plan {
   int has_bias = 1;
   float sp_beta = 50.f, sp_thr = 1.f;
   int64_t P = 0, ncols = 0, nparams = 0, ngrads = 0, max_rows = 0;
+  int64_t xld = 0;  // row stride of X in floats (P unless tr_plan_set_x_stride)
   FactorSet fs{};
   int ncu = 256;
   int W = 4;
@@ -125,7 +126,7 @@ extern "C" const char* tr_last_error(void) { return g_err.c_str(); }
 // prefetched row per resident workgroup), ties to the smaller workgroup.
 static void choose_fused(tr_plan* p) {
   p->fused = 0;
-  if (p->model != TR_MODEL_LINEAR || p->P % 4 != 0 || env_flag("TR_FORCE_TWOPASS")) return;
+  if (p->model != TR_MODEL_LINEAR || p->P % 4 != 0 || p->xld % 4 != 0 || env_flag("TR_FORCE_TWOPASS")) return;
   const int64_t P4 = p->P / 4;
   const size_t lds_max = 160 * 1024;
   const int Ts[5] = {64, 128, 256, 512, 1024};
@@ -193,6 +194,7 @@ extern "C" int tr_plan_create(tr_plan** out, int device, int model, int n_featur
     P *= feature_dims[k];
   }
   p->P = P;
+  p->xld = P;
   p->ncols = P * C;
   if (p->ncols >= ((int64_t)1 << 31)) {
     delete p;
@@ -337,6 +339,7 @@ extern "C" int tr_plan_create_spectral(tr_plan** out, int device, int64_t n_w, i
   p->sp_thr = softplus_threshold;
   p->max_rows = max_rows;
   p->P = g.WD;
+  p->xld = g.WD;
   p->nparams = g.nparams;
   p->ngrads = g.nparams + 1;
   FactorSet& fs = p->fs;
@@ -411,6 +414,44 @@ extern "C" int tr_plan_create_spectral(tr_plan** out, int device, int64_t n_w, i
   return 0;
 }
 
+// Row stride of X (strided / windowed views: row n starts at X + n*stride, its P floats
+// contiguous).  Vector (16-B) kernel paths need stride % 4 == 0 and a 16-B aligned X.
+extern "C" int tr_plan_set_x_stride(tr_plan* p, int64_t stride) {
+  if (p == nullptr) return fail(TR_E_ARG, "plan is NULL");
+  if (stride < 0) return fail(TR_E_ARG, "stride must be >= 0 (0 = dense rows)");
+  const int64_t x = stride == 0 ? p->P : stride;
+  p->xld = x;
+  if (p->model == TR_MODEL_SPECTRAL) {
+    p->sg.vec = (p->sg.WD % 4 == 0 && x % 4 == 0) ? 1 : 0;
+    return 0;
+  }
+  TR_HIP(hipSetDevice(p->device));
+  p->W = (p->P % 4 == 0 && x % 4 == 0) ? 4 : 1;
+  const int had_fused = p->fused;
+  const int64_t fgrid = p->fgrid;
+  choose_fused(p);
+  if (p->fused && (!had_fused || p->fgrid > fgrid)) {
+    // the workspace was carved for the creation-time strategy; keep within it
+    p->fused = had_fused;
+    p->fgrid = fgrid;
+  }
+  p->mfma_rows = (p->model == TR_MODEL_MULTINOMIAL && rows_mfma_supported(p->C, p->P) && x % 4 == 0 &&
+                  !env_flag("TR_NO_MFMA"))
+                     ? 1
+                     : 0;
+  return 0;
+}
+
+static bool x_vec_paths(const tr_plan* p) {
+  if (p->model == TR_MODEL_SPECTRAL) return p->sg.vec != 0;
+  return p->W == 4 || p->fused || p->mfma_rows;
+}
+static int check_x_align(const tr_plan* p, const float* X) {
+  if (X != nullptr && x_vec_paths(p) && (reinterpret_cast<uintptr_t>(X) & 15u) != 0)
+    return fail(TR_E_ARG, "X must be 16-byte aligned for this plan's vector kernels (or set a stride % 4 != 0)");
+  return 0;
+}
+
 extern "C" int tr_plan_destroy(tr_plan* p) {
   if (p == nullptr) return 0;
   (void)hipSetDevice(p->device);
@@ -447,7 +488,7 @@ static int spectral_forward(tr_plan* p, int mode, const float* X, int64_t n_rows
   }
   const int64_t rpw = (n_rows + p->sgrid - 1) / p->sgrid;
   TimedLaunch tl(p, st, TR_KERNEL_STREAM_FUSED);
-  TR_HIP(launch_spec_fused(mode, p->sg, p->sgrid, X, n_rows, p->phi, p->Phi0, weights, nullptr, 0.f, nullptr, 0,
+  TR_HIP(launch_spec_fused(mode, p->sg, p->sgrid, X, n_rows, p->xld, p->phi, p->Phi0, weights, nullptr, 0.f, nullptr, 0,
                            nullptr, out, rpw, 0, nullptr, st));
   return 0;
 }
@@ -458,6 +499,7 @@ extern "C" int tr_spectral_latents(tr_plan* p, const float* X, int64_t n_rows, c
   if (p->model != TR_MODEL_SPECTRAL) return fail(TR_E_ARG, "tr_spectral_latents needs a spectral plan");
   if (X == nullptr || params == nullptr || out == nullptr) return fail(TR_E_ARG, "NULL buffer");
   if (n_rows < 1 || p->sg.Rn < 1) return 0;
+  if (int rc0 = check_x_align(p, X)) return rc0;
   TR_HIP(hipSetDevice(p->device));
   return spectral_forward(p, SPEC_LATENT, X, n_rows, params, nullptr, out, (hipStream_t)stream);
 }
@@ -468,6 +510,7 @@ extern "C" int tr_forward(tr_plan* p, const float* X, int64_t n_rows, const floa
   if (X == nullptr || params == nullptr || weights == nullptr || out == nullptr)
     return fail(TR_E_ARG, "NULL buffer");
   if (n_rows < 1) return 0;
+  if (int rc0 = check_x_align(p, X)) return rc0;
   hipStream_t st = (hipStream_t)stream;
   TR_HIP(hipSetDevice(p->device));
   if (p->model == TR_MODEL_SPECTRAL) return spectral_forward(p, SPEC_PRED, X, n_rows, params, weights, out, st);
@@ -475,11 +518,11 @@ extern "C" int tr_forward(tr_plan* p, const float* X, int64_t n_rows, const floa
   if (rc) return rc;
   const int mode = p->model == TR_MODEL_LINEAR ? MODE_LIN_PRED : MODE_MNL_PRED;
   if (p->mfma_rows) {
-    TR_HIP(launch_rows_mfma(MODE_MNL_PRED, X, n_rows, p->P, p->dense, p->C, nullptr, nullptr, 0.f, out, nullptr,
+    TR_HIP(launch_rows_mfma(MODE_MNL_PRED, X, n_rows, p->P, p->xld, p->dense, p->C, nullptr, nullptr, 0.f, out, nullptr,
                             nullptr, st));
     return 0;
   }
-  TR_HIP(launch_rows(p->C, mode, p->W, X, n_rows, p->P, p->dense, params + p->fs.nfelem, nullptr, nullptr, 0.f,
+  TR_HIP(launch_rows(p->C, mode, p->W, X, n_rows, p->P, p->xld, p->dense, params + p->fs.nfelem, nullptr, nullptr, 0.f,
                      out, nullptr, nullptr, nullptr, st));
   return 0;
 }
@@ -494,6 +537,8 @@ extern "C" int tr_loss_grad(tr_plan* p, const float* X, int64_t n_rows, const vo
     return fail(TR_E_ARG, "multinomial model needs class_weight");
   if (n_rows < 0 || n_rows > p->max_rows) return fail(TR_E_ARG, "n_rows exceeds the plan's max_rows");
   if (!(norm > 0.0)) return fail(TR_E_ARG, "norm must be > 0");
+  if (n_rows > 0)
+    if (int rc0 = check_x_align(p, X)) return rc0;
   hipStream_t st = (hipStream_t)stream;
   TR_HIP(hipSetDevice(p->device));
   if (n_rows == 0) {
@@ -511,7 +556,7 @@ extern "C" int tr_loss_grad(tr_plan* p, const float* X, int64_t n_rows, const vo
     const int64_t rpw = (n_rows + p->sgrid - 1) / p->sgrid;
     {
       TimedLaunch tl(p, st, TR_KERNEL_STREAM_FUSED);
-      TR_HIP(launch_spec_fused(SPEC_TRAIN, p->sg, p->sgrid, X, n_rows, p->phi, p->Phi0, weights,
+      TR_HIP(launch_spec_fused(SPEC_TRAIN, p->sg, p->sgrid, X, n_rows, p->xld, p->phi, p->Phi0, weights,
                                (const float*)target, (float)(2.0 / norm), p->gpart, p->slab_stride, p->dpart, yhat_out,
                                rpw, reverse, stop_flag, st));
     }
@@ -535,12 +580,12 @@ extern "C" int tr_loss_grad(tr_plan* p, const float* X, int64_t n_rows, const vo
 
   if (p->fused) {
     if (yhat_out != nullptr)  // the single-pass kernel does not emit y_hat; one extra forward pass
-      TR_HIP(launch_rows(1, MODE_LIN_PRED, p->W, X, N, p->P, p->dense, bias, nullptr, nullptr, 0.f, yhat_out,
+      TR_HIP(launch_rows(1, MODE_LIN_PRED, p->W, X, N, p->P, p->xld, p->dense, bias, nullptr, nullptr, 0.f, yhat_out,
                          nullptr, nullptr, stop_flag, st));
     const int64_t rpw = (N + p->fgrid - 1) / p->fgrid;
     {
       TimedLaunch tl(p, st, TR_KERNEL_STREAM_FUSED);
-      TR_HIP(launch_linear_fused(p->fT, p->fCH, p->fgrid, X, N, p->P, p->dense, bias, (const float*)target,
+      TR_HIP(launch_linear_fused(p->fT, p->fCH, p->fgrid, X, N, p->P, p->xld, p->dense, bias, (const float*)target,
                                  (float)(2.0 / norm), p->gpart, p->dpart, yhat_out, rpw, reverse, stop_flag, st));
     }
     {
@@ -552,13 +597,13 @@ extern "C" int tr_loss_grad(tr_plan* p, const float* X, int64_t n_rows, const vo
     const int C = p->C;
     TimedLaunch* tl_rows = new TimedLaunch(p, st, TR_KERNEL_STREAM_ROWS);
     if (p->model == TR_MODEL_LINEAR) {
-      TR_HIP(launch_rows(1, MODE_LIN_TRAIN, p->W, X, N, p->P, p->dense, bias, target, nullptr,
+      TR_HIP(launch_rows(1, MODE_LIN_TRAIN, p->W, X, N, p->P, p->xld, p->dense, bias, target, nullptr,
                          (float)(2.0 / norm), p->rowbuf, p->dpart, yhat_out, stop_flag, st));
     } else if (p->mfma_rows) {
-      TR_HIP(launch_rows_mfma(MODE_MNL_TRAIN, X, N, p->P, p->dense, C, (const int64_t*)target, class_weight,
+      TR_HIP(launch_rows_mfma(MODE_MNL_TRAIN, X, N, p->P, p->xld, p->dense, C, (const int64_t*)target, class_weight,
                               (float)(1.0 / norm), p->rowbuf, p->dpart, stop_flag, st));
     } else {
-      TR_HIP(launch_rows(C, MODE_MNL_TRAIN, p->W, X, N, p->P, p->dense, nullptr, target, class_weight,
+      TR_HIP(launch_rows(C, MODE_MNL_TRAIN, p->W, X, N, p->P, p->xld, p->dense, nullptr, target, class_weight,
                          (float)(1.0 / norm), p->rowbuf, p->dpart, nullptr, stop_flag, st));
     }
     delete tl_rows;
@@ -575,7 +620,7 @@ extern "C" int tr_loss_grad(tr_plan* p, const float* X, int64_t n_rows, const vo
     nchunks = (N + rpc - 1) / rpc;
     {
       TimedLaunch tl(p, st, TR_KERNEL_STREAM_COLS);
-      TR_HIP(launch_cols(C, p->W, nstripes, nchunks, X, N, p->P, p->rowbuf, rpc, p->gpart, 1, stop_flag, st));
+      TR_HIP(launch_cols(C, p->W, nstripes, nchunks, X, N, p->P, p->xld, p->rowbuf, rpc, p->gpart, 1, stop_flag, st));
     }
     {
       TimedLaunch tl(p, st, TR_KERNEL_REDUCE);

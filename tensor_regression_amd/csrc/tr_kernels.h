@@ -32,13 +32,15 @@ struct UpdateArgs {
 };
 
 // Launch helpers (all asynchronous on `st`).  Return hipError_t of the launch.
+// `xld` is X's row stride in floats (P for a dense X; may differ for strided / windowed views,
+// the P floats of each row being contiguous).
 hipError_t launch_prep_factors(const FactorSet& fs, const float* params, float beta, float thr,
                                float* phi, float* dphi, const int32_t* stop, hipStream_t st);
 // softplus + dense B (one launch when the factors fit LDS, else prep + build)
 hipError_t launch_build_dense(const FactorSet& fs, const float* params, float beta, float thr, float* phi,
                               float* dphi, const float* w, float* dense, const int32_t* stop, hipStream_t st);
 bool linear_fused_supported(int T, int CH);
-hipError_t launch_linear_fused(int T, int CH, int grid, const float* X, int64_t N, int64_t P,
+hipError_t launch_linear_fused(int T, int CH, int grid, const float* X, int64_t N, int64_t P, int64_t xld,
                                const float* B, const float* bias, const float* y, float scale,
                                float* gpart, double* dpart, float* yhat, int64_t rows_per_wg,
                                int reverse, const int32_t* stop, hipStream_t st);
@@ -46,18 +48,18 @@ hipError_t prepare_linear_fused(int T, int CH, size_t lds_bytes, int* wg_per_cu)
 int rows_rb(int C);
 int cols_cw(int C);
 bool rows_supported(int C);
-hipError_t launch_rows(int C, int mode, int W, const float* X, int64_t N, int64_t P,
+hipError_t launch_rows(int C, int mode, int W, const float* X, int64_t N, int64_t P, int64_t xld,
                        const float* Bt, const float* bias, const void* target, const float* class_w,
                        float scale, float* out, double* dpart, float* yhat, const int32_t* stop,
                        hipStream_t st);
 int64_t rows_num_waves(int C, int64_t N);
 bool rows_mfma_supported(int C, int64_t P);
 int64_t rows_mfma_num_waves(int64_t N);
-hipError_t launch_rows_mfma(int mode, const float* X, int64_t N, int64_t P, const float* Bt, int C,
+hipError_t launch_rows_mfma(int mode, const float* X, int64_t N, int64_t P, int64_t xld, const float* Bt, int C,
                             const int64_t* lab, const float* class_w, float scale, float* out, double* dpart,
                             const int32_t* stop, hipStream_t st);
 hipError_t launch_cols(int C, int W, int64_t nstripes, int64_t nchunks, const float* X, int64_t N,
-                       int64_t P, const float* V, int64_t rows_per_chunk, float* gpart, int reverse,
+                       int64_t P, int64_t xld, const float* V, int64_t rows_per_chunk, float* gpart, int reverse,
                        const int32_t* stop, hipStream_t st);
 hipError_t launch_reduce_slabs(int W, const float* part, int64_t nslabs, int64_t ncols, float* out,
                                const double* dpart, int64_t nd, double loss_scale, float* loss_slot,

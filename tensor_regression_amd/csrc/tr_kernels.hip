@@ -157,7 +157,7 @@ __global__ __launch_bounds__(256) void k_build_dense(FactorSet fs, const float* 
 // ==========================================================================================
 template <int T, int CH>
 __global__ __launch_bounds__(T) void k_linear_fused(
-    const float* __restrict__ X, int64_t N, int64_t P, const float* __restrict__ B,
+    const float* __restrict__ X, int64_t N, int64_t P, int64_t xld, const float* __restrict__ B,
     const float* __restrict__ bias_p, const float* __restrict__ y, float scale,
     float* __restrict__ gpart, double* __restrict__ dpart, float* __restrict__ yhat,
     int64_t rows_per_wg, int reverse, const int32_t* __restrict__ stop) {
@@ -191,7 +191,7 @@ __global__ __launch_bounds__(T) void k_linear_fused(
 
   auto row_of = [&](int64_t i) -> int64_t { return reverse ? (r1 - 1 - i) : (r0 + i); };
   auto load = [&](float4(&x)[CH], int64_t i) {
-    const char* base = Xb + row_of(i) * (int64_t)row_bytes;
+    const char* base = Xb + row_of(i) * xld * 4;  // row stride xld floats (>= or < P: windowed views)
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<char*>(base), (short)0, (int)row_bytes, 0x00020000);
 #pragma unroll
@@ -276,7 +276,7 @@ template <> struct VecT<1> {
 
 template <int C, int RB, int MODE, int W>
 __global__ __launch_bounds__(256) void k_rows(
-    const float* __restrict__ X, int64_t N, int64_t P, const float* __restrict__ Bt,
+    const float* __restrict__ X, int64_t N, int64_t P, int64_t xld, const float* __restrict__ Bt,
     const float* __restrict__ bias_p, const void* __restrict__ target,
     const float* __restrict__ class_w, float scale, float* __restrict__ out,
     double* __restrict__ dpart, float* __restrict__ yhat, const int32_t* __restrict__ stop) {
@@ -302,7 +302,7 @@ __global__ __launch_bounds__(256) void k_rows(
 #pragma unroll
   for (int r = 0; r < RB; ++r) {
     const int64_t row = (row0 + r < N) ? row0 + r : N - 1;
-    xr[r] = Xv + row * PW;
+    xr[r] = Xv + row * (xld / W);
   }
   float acc[RB][C];
 #pragma unroll
@@ -474,7 +474,7 @@ typedef float tr_f32x4 __attribute__((ext_vector_type(4)));
 
 template <int MODE, int RT>
 __global__ __launch_bounds__(256) void k_rows_mfma(
-    const float* __restrict__ X, int64_t N, int64_t P, const float* __restrict__ Bt, int C,
+    const float* __restrict__ X, int64_t N, int64_t P, int64_t xld, const float* __restrict__ Bt, int C,
     const int64_t* __restrict__ lab, const float* __restrict__ class_w, float scale,
     float* __restrict__ out, double* __restrict__ dpart, const int32_t* __restrict__ stop) {
   if (stop != nullptr && *stop != 0) return;
@@ -495,7 +495,7 @@ __global__ __launch_bounds__(256) void k_rows_mfma(
   for (int rt = 0; rt < RT; ++rt) {
     int64_t r = row0 + rt * 16 + i;
     r = r < N ? r : N - 1;
-    xr[rt] = reinterpret_cast<const float4*>(X + r * P + 8 * g);
+    xr[rt] = reinterpret_cast<const float4*>(X + r * xld + 8 * g);
   }
   const bool cls_ok = i < C;
   // Bt is padded to 16 class rows (rows >= C are zero): unconditional loads, no per-lane branches
@@ -591,7 +591,7 @@ __global__ __launch_bounds__(256) void k_rows_mfma(
 // streamed last (still in the Infinity Cache) are read first.
 // ==========================================================================================
 template <int C, int CW, int W>
-__global__ __launch_bounds__(256) void k_cols(const float* __restrict__ X, int64_t N, int64_t P,
+__global__ __launch_bounds__(256) void k_cols(const float* __restrict__ X, int64_t N, int64_t P, int64_t xld,
                                               const float* __restrict__ Vw, int64_t rows_per_chunk,
                                               float* __restrict__ gpart, int reverse,
                                               const int32_t* __restrict__ stop) {
@@ -600,6 +600,7 @@ __global__ __launch_bounds__(256) void k_cols(const float* __restrict__ X, int64
   if (stop != nullptr && *stop != 0) return;
   const int t = threadIdx.x;
   const int64_t PW = P / W;
+  const int64_t LDW = xld / W;  // row stride in vectors
   const int64_t k = reverse ? (int64_t)(gridDim.y - 1 - blockIdx.y) : (int64_t)blockIdx.y;
   const int64_t n0 = k * rows_per_chunk;
   const int64_t n1 = n0 + rows_per_chunk < N ? n0 + rows_per_chunk : N;
@@ -625,7 +626,7 @@ __global__ __launch_bounds__(256) void k_cols(const float* __restrict__ X, int64
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int j = 0; j < CW; ++j) x[u][j] = ldx(Xv + (n + u) * PW + col[j]);
+      for (int j = 0; j < CW; ++j) x[u][j] = ldx(Xv + (n + u) * LDW + col[j]);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
 #pragma unroll
@@ -639,7 +640,7 @@ __global__ __launch_bounds__(256) void k_cols(const float* __restrict__ X, int64
   for (; n < n1; ++n) {
     VT x[CW];
 #pragma unroll
-    for (int j = 0; j < CW; ++j) x[j] = ldx(Xv + n * PW + col[j]);
+    for (int j = 0; j < CW; ++j) x[j] = ldx(Xv + n * LDW + col[j]);
 #pragma unroll
     for (int c = 0; c < C; ++c) {
       const float v = Vw[n * C + c];
@@ -1056,17 +1057,17 @@ hipError_t launch_build_dense(const FactorSet& fs, const float* params, float be
   X(1024, 1) X(1024, 2) X(1024, 3) X(1024, 4) X(1024, 5) X(1024, 6) X(1024, 7) X(1024, 8)
 
 template <int T, int CH>
-static hipError_t fused_launch_t(int grid, const float* X, int64_t N, int64_t P, const float* B,
+static hipError_t fused_launch_t(int grid, const float* X, int64_t N, int64_t P, int64_t xld, const float* B,
                                  const float* bias, const float* y, float scale, float* gpart,
                                  double* dpart, float* yhat, int64_t rpw, int reverse,
                                  const int32_t* stop, hipStream_t st) {
   const size_t lds = (size_t)P * sizeof(float) + 2 * (T / TR_WAVE) * sizeof(float);
-  hipLaunchKernelGGL((k_linear_fused<T, CH>), dim3(grid), dim3(T), lds, st, X, N, P, B, bias, y,
+  hipLaunchKernelGGL((k_linear_fused<T, CH>), dim3(grid), dim3(T), lds, st, X, N, P, xld, B, bias, y,
                      scale, gpart, dpart, yhat, rpw, reverse, stop);
   return hipGetLastError();
 }
 
-typedef hipError_t (*fused_fn_t)(int, const float*, int64_t, int64_t, const float*, const float*,
+typedef hipError_t (*fused_fn_t)(int, const float*, int64_t, int64_t, int64_t, const float*, const float*,
                                  const float*, float, float*, double*, float*, int64_t, int,
                                  const int32_t*, hipStream_t);
 struct FusedEntry {
@@ -1087,13 +1088,13 @@ static const FusedEntry* find_fused(int T, int CH) {
 
 bool linear_fused_supported(int T, int CH) { return find_fused(T, CH) != nullptr; }
 
-hipError_t launch_linear_fused(int T, int CH, int grid, const float* X, int64_t N, int64_t P,
+hipError_t launch_linear_fused(int T, int CH, int grid, const float* X, int64_t N, int64_t P, int64_t xld,
                                const float* B, const float* bias, const float* y, float scale,
                                float* gpart, double* dpart, float* yhat, int64_t rows_per_wg,
                                int reverse, const int32_t* stop, hipStream_t st) {
   const FusedEntry* e = find_fused(T, CH);
   if (e == nullptr) return hipErrorInvalidValue;
-  return e->launch(grid, X, N, P, B, bias, y, scale, gpart, dpart, yhat, rows_per_wg, reverse, stop, st);
+  return e->launch(grid, X, N, P, xld, B, bias, y, scale, gpart, dpart, yhat, rows_per_wg, reverse, stop, st);
 }
 
 // Sets the dynamic-LDS limit and reports spill-free occupancy (workgroups per CU; 0 = unusable).
@@ -1121,24 +1122,24 @@ bool rows_supported(int C) { return C >= 1 && C <= 16; }
 int64_t rows_num_waves(int C, int64_t N) { return (N + rows_rb(C) - 1) / rows_rb(C); }
 
 template <int C, int MODE, int W>
-static hipError_t rows_launch_t(const float* X, int64_t N, int64_t P, const float* Bt, const float* bias,
+static hipError_t rows_launch_t(const float* X, int64_t N, int64_t P, int64_t xld, const float* Bt, const float* bias,
                                 const void* target, const float* class_w, float scale, float* out,
                                 double* dpart, float* yhat, const int32_t* stop, hipStream_t st) {
   constexpr int RB = (C == 1) ? 8 : 4;
   const int64_t waves = (N + RB - 1) / RB;
   const unsigned grid = cdiv(waves, 4);
-  hipLaunchKernelGGL((k_rows<C, RB, MODE, W>), dim3(grid), dim3(256), 0, st, X, N, P, Bt, bias, target,
+  hipLaunchKernelGGL((k_rows<C, RB, MODE, W>), dim3(grid), dim3(256), 0, st, X, N, P, xld, Bt, bias, target,
                      class_w, scale, out, dpart, yhat, stop);
   return hipGetLastError();
 }
 
 template <int C>
-static hipError_t rows_launch_c(int mode, int W, const float* X, int64_t N, int64_t P, const float* Bt,
+static hipError_t rows_launch_c(int mode, int W, const float* X, int64_t N, int64_t P, int64_t xld, const float* Bt,
                                 const float* bias, const void* target, const float* class_w, float scale,
                                 float* out, double* dpart, float* yhat, const int32_t* stop,
                                 hipStream_t st) {
 #define TR_ROWS(MODE, WW) \
-  rows_launch_t<C, MODE, WW>(X, N, P, Bt, bias, target, class_w, scale, out, dpart, yhat, stop, st)
+  rows_launch_t<C, MODE, WW>(X, N, P, xld, Bt, bias, target, class_w, scale, out, dpart, yhat, stop, st)
   if (C == 1 && mode == MODE_LIN_TRAIN) return W == 4 ? TR_ROWS(MODE_LIN_TRAIN, 4) : TR_ROWS(MODE_LIN_TRAIN, 1);
   if (C == 1 && mode == MODE_LIN_PRED) return W == 4 ? TR_ROWS(MODE_LIN_PRED, 4) : TR_ROWS(MODE_LIN_PRED, 1);
   if (mode == MODE_MNL_TRAIN) return W == 4 ? TR_ROWS(MODE_MNL_TRAIN, 4) : TR_ROWS(MODE_MNL_TRAIN, 1);
@@ -1156,11 +1157,11 @@ static hipError_t rows_launch_c(int mode, int W, const float* X, int64_t N, int6
     default: break;      \
   }
 
-hipError_t launch_rows(int C, int mode, int W, const float* X, int64_t N, int64_t P, const float* Bt,
+hipError_t launch_rows(int C, int mode, int W, const float* X, int64_t N, int64_t P, int64_t xld, const float* Bt,
                        const float* bias, const void* target, const float* class_w, float scale,
                        float* out, double* dpart, float* yhat, const int32_t* stop, hipStream_t st) {
 #define TR_CALL_ROWS(CC) \
-  rows_launch_c<CC>(mode, W, X, N, P, Bt, bias, target, class_w, scale, out, dpart, yhat, stop, st)
+  rows_launch_c<CC>(mode, W, X, N, P, xld, Bt, bias, target, class_w, scale, out, dpart, yhat, stop, st)
   TR_C_CASES(TR_CALL_ROWS)
 #undef TR_CALL_ROWS
   return hipErrorInvalidValue;
@@ -1171,16 +1172,16 @@ static const int kMfmaRT = 2;
 bool rows_mfma_supported(int C, int64_t P) { return C >= 1 && C <= 16 && P % 32 == 0; }
 int64_t rows_mfma_num_waves(int64_t N) { return (N + 16 * kMfmaRT - 1) / (16 * kMfmaRT); }
 
-hipError_t launch_rows_mfma(int mode, const float* X, int64_t N, int64_t P, const float* Bt, int C,
+hipError_t launch_rows_mfma(int mode, const float* X, int64_t N, int64_t P, int64_t xld, const float* Bt, int C,
                             const int64_t* lab, const float* class_w, float scale, float* out, double* dpart,
                             const int32_t* stop, hipStream_t st) {
   const int64_t waves = rows_mfma_num_waves(N);
   const unsigned grid = cdiv(waves, 4);
   if (mode == MODE_MNL_TRAIN)
-    hipLaunchKernelGGL((k_rows_mfma<MODE_MNL_TRAIN, kMfmaRT>), dim3(grid), dim3(256), 0, st, X, N, P, Bt, C, lab,
+    hipLaunchKernelGGL((k_rows_mfma<MODE_MNL_TRAIN, kMfmaRT>), dim3(grid), dim3(256), 0, st, X, N, P, xld, Bt, C, lab,
                        class_w, scale, out, dpart, stop);
   else if (mode == MODE_MNL_PRED)
-    hipLaunchKernelGGL((k_rows_mfma<MODE_MNL_PRED, kMfmaRT>), dim3(grid), dim3(256), 0, st, X, N, P, Bt, C, lab,
+    hipLaunchKernelGGL((k_rows_mfma<MODE_MNL_PRED, kMfmaRT>), dim3(grid), dim3(256), 0, st, X, N, P, xld, Bt, C, lab,
                        class_w, scale, out, dpart, stop);
   else
     return hipErrorInvalidValue;
@@ -1189,21 +1190,21 @@ hipError_t launch_rows_mfma(int mode, const float* X, int64_t N, int64_t P, cons
 
 // ---- two-pass backward columns -------------------------------------------------------------
 template <int C, int W>
-static hipError_t cols_launch_t(int64_t nstripes, int64_t nchunks, const float* X, int64_t N, int64_t P,
+static hipError_t cols_launch_t(int64_t nstripes, int64_t nchunks, const float* X, int64_t N, int64_t P, int64_t xld,
                                 const float* V, int64_t rpc, float* gpart, int reverse,
                                 const int32_t* stop, hipStream_t st) {
   constexpr int CW = (C == 1) ? 4 : (C == 2 ? 2 : 1);
   hipLaunchKernelGGL((k_cols<C, CW, W>), dim3((unsigned)nstripes, (unsigned)nchunks), dim3(256), 0, st,
-                     X, N, P, V, rpc, gpart, reverse, stop);
+                     X, N, P, xld, V, rpc, gpart, reverse, stop);
   return hipGetLastError();
 }
 
 hipError_t launch_cols(int C, int W, int64_t nstripes, int64_t nchunks, const float* X, int64_t N,
-                       int64_t P, const float* V, int64_t rows_per_chunk, float* gpart, int reverse,
+                       int64_t P, int64_t xld, const float* V, int64_t rows_per_chunk, float* gpart, int reverse,
                        const int32_t* stop, hipStream_t st) {
 #define TR_CALL_COLS(CC)                                                                           \
-  (W == 4 ? cols_launch_t<CC, 4>(nstripes, nchunks, X, N, P, V, rows_per_chunk, gpart, reverse, stop, st) \
-          : cols_launch_t<CC, 1>(nstripes, nchunks, X, N, P, V, rows_per_chunk, gpart, reverse, stop, st))
+  (W == 4 ? cols_launch_t<CC, 4>(nstripes, nchunks, X, N, P, xld, V, rows_per_chunk, gpart, reverse, stop, st) \
+          : cols_launch_t<CC, 1>(nstripes, nchunks, X, N, P, xld, V, rows_per_chunk, gpart, reverse, stop, st))
   TR_C_CASES(TR_CALL_COLS)
 #undef TR_CALL_COLS
   return hipErrorInvalidValue;

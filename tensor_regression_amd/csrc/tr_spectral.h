@@ -54,7 +54,8 @@ hipError_t launch_spec_prep(const SpecGeom& g, const float* params, float beta, 
 //                `out` (optional) receives the fit-model y_hat (N x NO)
 //   SPEC_PRED  : out (N x NO) = lin_model + spectral_model (the reference's predict)
 //   SPEC_LATENT: out (N x Rn) = stepwise_latents_model
-hipError_t launch_spec_fused(int mode, const SpecGeom& g, int grid, const float* X, int64_t N, const float* phi,
+hipError_t launch_spec_fused(int mode, const SpecGeom& g, int grid, const float* X, int64_t N, int64_t xld,
+                             const float* phi,
                              const float* Phi0, const float* wts, const float* y, float scale, float* slab,
                              int64_t slab_stride, double* dpart, float* out, int64_t rows_per_wg, int reverse,
                              const int32_t* stop, hipStream_t st);

@@ -150,7 +150,7 @@ __device__ __forceinline__ void spec_wait_vm(int n) {
 // ------------------------------------------------------------------------------------------
 template <int MODE, int WSMAX, int KT>
 __global__ __launch_bounds__(kSpecT) void k_spec_fused(
-    const float* __restrict__ X, int64_t N, SpecGeom g, const float* __restrict__ phi,
+    const float* __restrict__ X, int64_t N, int64_t xld, SpecGeom g, const float* __restrict__ phi,
     const float* __restrict__ Phi0, const float* __restrict__ wts, const float* __restrict__ y, float scale,
     float* __restrict__ slab, int64_t slab_stride, double* __restrict__ dpart, float* __restrict__ out,
     int64_t rows_per_wg, int reverse, const int32_t* __restrict__ stop) {
@@ -253,7 +253,7 @@ __global__ __launch_bounds__(kSpecT) void k_spec_fused(
     const int64_t r0 = (int64_t)p * RB * D;
     int64_t r1 = (int64_t)(p + 1) * RB * D;
     if (r1 > g.WD) r1 = g.WD;
-    const float* src = X + n * g.WD;
+    const float* src = X + n * xld;
     int cnt = 0;
     if (g.vec) {
       const int64_t a = r0 >> 2, b = r1 >> 2;  // float4 range (RB*D and W*D are multiples of 4)
@@ -847,12 +847,12 @@ bool spec_geom_init(SpecGeom* g, int64_t W, int64_t D, int64_t NO, int Rn, int R
 template <int MODE, int WSMAX, int KT>
 struct SpecInst {
   static const void* ptr() { return reinterpret_cast<const void*>(&k_spec_fused<MODE, WSMAX, KT>); }
-  static hipError_t launch(const SpecGeom& g, int grid, const float* X, int64_t N, const float* phi,
+  static hipError_t launch(const SpecGeom& g, int grid, const float* X, int64_t N, int64_t xld, const float* phi,
                            const float* Phi0, const float* wts, const float* y, float scale, float* slab,
                            int64_t slab_stride, double* dpart, float* out, int64_t rpw, int reverse,
                            const int32_t* stop, hipStream_t st) {
     hipLaunchKernelGGL((k_spec_fused<MODE, WSMAX, KT>), dim3(grid), dim3(kSpecT), (size_t)g.lds_floats * 4, st,
-                       X, N, g, phi, Phi0, wts, y, scale, slab, slab_stride, dpart, out, rpw, reverse, stop);
+                       X, N, xld, g, phi, Phi0, wts, y, scale, slab, slab_stride, dpart, out, rpw, reverse, stop);
     return hipGetLastError();
   }
 };
@@ -907,11 +907,12 @@ hipError_t launch_spec_prep(const SpecGeom& g, const float* params, float beta, 
   return hipGetLastError();
 }
 
-hipError_t launch_spec_fused(int mode, const SpecGeom& g, int grid, const float* X, int64_t N, const float* phi,
+hipError_t launch_spec_fused(int mode, const SpecGeom& g, int grid, const float* X, int64_t N, int64_t xld,
+                             const float* phi,
                              const float* Phi0, const float* wts, const float* y, float scale, float* slab,
                              int64_t slab_stride, double* dpart, float* out, int64_t rows_per_wg, int reverse,
                              const int32_t* stop, hipStream_t st) {
-return spec_dispatch<SpecLaunch>(g, mode, g, grid, X, N, phi, Phi0, wts, y, scale, slab, slab_stride, dpart, out,
+return spec_dispatch<SpecLaunch>(g, mode, g, grid, X, N, xld, phi, Phi0, wts, y, scale, slab, slab_stride, dpart, out,
                                    rows_per_wg, reverse, stop, st);
 }
 

@@ -81,7 +81,7 @@ def model(X, Bcp, weights, non_negative, softplus_kwargs=None):
     plan = _plan_for(_lib.TR_MODEL_MULTINOMIAL, X.shape[1:], C, rank, 1, non_negative, softplus_kwargs, dev)
     arena = plan.pack([torch.as_tensor(A).to(dev) for A in Bcp])
     w = torch.as_tensor(weights, dtype=torch.float32).to(dev).contiguous()
-    return plan.forward(as_device_f32(X, dev.index), arena, w)
+    return plan.forward(_engine.as_device_rows(X, dev.index), arena, w)
 
 
 ####################################
@@ -128,7 +128,7 @@ class CP_logistic_regression():
         dev = _engine.compute_device(self.X, self.device)
         c = self._dev_cache
         if c is None or c[0] != dev or c[1] is not self.X or c[2] is not self.y:
-            Xd = as_device_f32(self.X, dev)
+            Xd = _engine.as_device_rows(self.X, dev)
             yd = self.y.to(f"cuda:{dev}", torch.long).contiguous()
             C = int(self.Bcp[-1].shape[0])
             ymin, ymax = int(yd.min().item()), int(yd.max().item())
@@ -252,7 +252,7 @@ class CP_logistic_regression():
             for ii in range(len(Bcp)):
                 Bcp[ii] = Bcp[ii].to(device)
         dev = _engine.compute_device(X, device)
-        Xd = as_device_f32(X, dev)
+        Xd = _engine.as_device_rows(X, dev)
         logit = model(Xd, [torch.as_tensor(A).to(f"cuda:{dev}") for A in Bcp], self.weights, self.non_negative,
                       softplus_kwargs=self.softplus_kwargs).detach().cpu().numpy()
         pred = np.argmax(logit, axis=1)

@@ -98,7 +98,7 @@ def _zero_factors(shapes, dev):
 def _module_forward(X, Bcp_n, Bcp_c, weights, rank_normal, non_negative, bias, softplus_kwargs, what):
     """Runs the predict kernel with one side of the model empty (rank 0 => that term is absent)."""
     dev = X.device
-    Xd = as_device_f32(X, dev.index)
+    Xd = _engine.as_device_rows(X, dev.index)
     W, D = int(X.shape[1]), int(X.shape[2])
     bias = torch.as_tensor(bias, dtype=torch.float32).to(dev).reshape(-1)
     n_out = int((Bcp_n or Bcp_c)[2].shape[0])
@@ -256,13 +256,17 @@ class CP_linear_regression():
         return W, D, O, int(self.Bcp_n[0].shape[1]), int(self.Bcp_c[0].shape[1]), int(self.Bcp_c[0].shape[2])
 
     def _get_plan(self, X, rows):
+        from .util import HostStream
+        if isinstance(X, HostStream):
+            rows = min(rows, X.chunk_rows)
         W, D, O, Rn, Rs, Cc = self._shape()
-        if X.ndim != 3 or (int(X.shape[1]), int(X.shape[2])) != (W, D):
+        if len(X.shape) != 3 or (int(X.shape[1]), int(X.shape[2])) != (W, D):
             raise ValueError(f"X must be (N, {W}, {D}) for these factors; got {tuple(X.shape)}")
         p = self._plan
         if (p is None or p.max_rows < rows or p.dims != (W, D, O)
                 or (p.rank_normal, p.rank_spectral, p.n_complex) != (Rn, Rs, Cc)):
-            p = SpectralPlan(W, D, O, Rn, Rs, Cc, rows, self.non_negative, self.softplus_kwargs, X.device)
+            p = SpectralPlan(W, D, O, Rn, Rs, Cc, rows, self.non_negative, self.softplus_kwargs,
+                             X.device if isinstance(X, torch.Tensor) else X.dev_index)
             self._plan = p
         return p
 
@@ -270,8 +274,12 @@ class CP_linear_regression():
         if self.dtype != torch.float32:
             raise NotImplementedError(f"the gfx950 kernels compute in fp32; this model was built with "
                                       f"dtype={self.dtype}")
-        dev = _engine.compute_device(X, self.device)
-        X = as_device_f32(X, dev)
+        from .util import HostStream
+        if isinstance(X, HostStream):
+            dev = X.dev_index
+        else:
+            dev = _engine.compute_device(X, self.device)
+            X = _engine.as_device_rows(X, dev)
         y = torch.as_tensor(y)
         O = int(self.Bcp_n[2].shape[0])
         if y.ndim != 2 or y.shape[0] != X.shape[0] or y.shape[1] != O:
@@ -303,6 +311,9 @@ class CP_linear_regression():
         if LBFGS_kwargs is None:
             raise TypeError("torch.optim.lbfgs.LBFGS() argument after ** must be a mapping, not NoneType")
         X, y, dev = self._inputs(X, y)
+        from .util import HostStream
+        if isinstance(X, HostStream):
+            raise NotImplementedError("the LBFGS fit needs X resident on the device (use fit_Adam for a HostStream)")
         N, O = X.shape[0], y.shape[1]
         plan = self._get_plan(X, N)
         optimizer = torch.optim.LBFGS(list(self.Bcp_n) + list(self.Bcp_c) + [self.bias], **LBFGS_kwargs)
@@ -368,6 +379,9 @@ class CP_linear_regression():
         norm = n_global * y.shape[1]
         arena = self._arena(plan)
         w = self._weights(dev)
+        from .util import HostStream
+        if verbose in (2, 3) and isinstance(X, HostStream):
+            raise NotImplementedError("verbose=2/3 (per-iteration y_hat variance) is not offered for a HostStream X")
         vcb = _VerbosePrinter(plan, X, y, w, norm) if verbose in (2, 3) else None
         convergence_reached, _ = run_adam_fit(plan, X, y, None, norm, arena, w, lambda_L2, max_iter, tol, patience,
                                               hp, self.loss_running, verbose_cb=vcb, allreduce=allreduce)
@@ -399,7 +413,7 @@ class CP_linear_regression():
             X = torch.tensor(X, dtype=torch.float32, requires_grad=False)
         Bcp_n, Bcp_c = self._factors_for(Bcp, device)
         dev = _engine.compute_device(X, device)
-        Xd = as_device_f32(X, dev)
+        Xd = _engine.as_device_rows(X, dev)
         plan = self._get_plan(Xd, Xd.shape[0])
         arena = plan.pack(Bcp_n, Bcp_c, self.bias)
         y_hat = plan.forward(Xd, arena, self._weights(dev))
@@ -413,7 +427,7 @@ class CP_linear_regression():
             X = torch.tensor(X, dtype=torch.float32, requires_grad=False)
         Bcp_n, Bcp_c = self._factors_for(Bcp, device)
         dev = _engine.compute_device(X, device)
-        Xd = as_device_f32(X, dev)
+        Xd = _engine.as_device_rows(X, dev)
         if int(Bcp_n[0].shape[1]) == 0:
             return torch.zeros(1).numpy()
         plan = self._get_plan(Xd, Xd.shape[0])

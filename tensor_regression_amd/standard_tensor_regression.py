@@ -84,7 +84,7 @@ def lin_model(X, Bcp, weights, non_negative, bias, softplus_kwargs=None):
                          f"tensor_1.shape={list(X.shape)}, factors={[tuple(A.shape) for A in Bcp]}")
     rank = int(Bcp[0].shape[1])
     dev = X.device
-    Xd = as_device_f32(X, dev.index)
+    Xd = _engine.as_device_rows(X, dev.index)
     plan = _plan_for(_lib.TR_MODEL_LINEAR, X.shape[1:], 1, rank, 1, non_negative, softplus_kwargs, dev)
     arena = plan.pack([torch.as_tensor(A).to(dev) for A in Bcp], torch.as_tensor(bias).to(dev))
     w = torch.as_tensor(weights, dtype=torch.float32).to(dev).contiguous()
@@ -178,6 +178,9 @@ class CP_linear_regression():
                                       f"dtype={self.dtype}")
 
     def _get_plan(self, X, rows):
+        from .util import HostStream
+        if isinstance(X, HostStream):
+            rows = min(rows, X.chunk_rows)
         dims = [int(A.shape[0]) for A in self.Bcp]
         if list(X.shape[1:]) != dims:
             raise ValueError(f"Incorrect shapes for inner product along {len(dims)} common modes. "
@@ -185,14 +188,21 @@ class CP_linear_regression():
         p = self._plan
         if p is None or p.max_rows < rows or p.feature_dims != dims or p.rank != int(self.Bcp[0].shape[1]):
             p = Plan(_lib.TR_MODEL_LINEAR, dims, 1, int(self.Bcp[0].shape[1]), rows, self.non_negative,
-                     self.softplus_kwargs, X.device)
+                     self.softplus_kwargs, X.device if isinstance(X, torch.Tensor) else X.dev_index)
             self._plan = p
         return p
 
     def _inputs(self, X, y):
         self._check_fp32()
+        from .util import HostStream
+        if isinstance(X, HostStream):  # out-of-core: X streams from host memory every iteration
+            dev = X.dev_index
+            y = torch.as_tensor(y)
+            if y.ndim != 1 or y.shape[0] != len(X):
+                raise ValueError(f"y must be 1-D with len(y) == len(X); got y.shape={tuple(y.shape)}")
+            return X, as_device_f32(y, dev), dev
         dev = _engine.compute_device(X, self.device)
-        X = as_device_f32(X, dev)
+        X = _engine.as_device_rows(X, dev)
         y = torch.as_tensor(y)
         if y.ndim != 1 or y.shape[0] != X.shape[0]:
             raise ValueError(f"y must be 1-D with len(y) == X.shape[0]; got y.shape={tuple(y.shape)}, "
@@ -208,6 +218,9 @@ class CP_linear_regression():
         if LBFGS_kwargs is None:
             raise TypeError("torch.optim.lbfgs.LBFGS() argument after ** must be a mapping, not NoneType")
         X, y, dev = self._inputs(X, y)
+        from .util import HostStream
+        if isinstance(X, HostStream):
+            raise NotImplementedError("the LBFGS fit needs X resident on the device (use fit_Adam for a HostStream)")
         N = X.shape[0]
         plan = self._get_plan(X, N)
         params = self.Bcp + [self.bias]
@@ -252,6 +265,8 @@ class CP_linear_regression():
                  Adam_kwargs=None, process_group=None):
         """Adam fit (standard_tensor_regression.py:400-476), device resident on gfx950.
 
+        X: a device tensor (samples may be a strided / windowed view, util.windowed_view) or a
+        util.HostStream (host-resident X streamed through HBM in chunks every iteration).
         process_group: optional torch.distributed group; X / y are then this rank's sample
         shard and the per-iteration gradient arena is summed with one all-reduce.
         """
@@ -259,6 +274,9 @@ class CP_linear_regression():
         X, y, dev = self._inputs(X, y)
         plan = self._get_plan(X, X.shape[0])
         n_global = float(X.shape[0])
+        from .util import HostStream
+        if verbose == 2 and isinstance(X, HostStream):
+            raise NotImplementedError("verbose=2 (per-iteration y_hat variance) is not offered for a HostStream X")
         allreduce = None
         if process_group is not None:
             import torch.distributed as dist
