@@ -47,6 +47,10 @@ CONFIGS = {
                         "reference rejects complex X; |rfft|-like non-negative synthetic data), rank_normal = "
                         "rank_spectral = 8, n_complex_dim 1, y (32768, 2), Adam lr 0.01"),
 }
+CONFIGS["c6"] = dict(kind="linear", rows=65536, dims=(256, 128), rank=8, windowed=True,
+                     workload="windowed variant of configs[1] (util.py:67-114 WindowedDataset): 65536 windows of "
+                              "256 x 128 over an untiled (65791, 128) fp32 series, read in place through the row "
+                              "stride (no materialised windows), rank 8, Adam lr 0.01")
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32 = the fp32 vector rate
 
 
@@ -58,7 +62,13 @@ def make_data(cfg, rank_id, dev):
     """Seeded synthetic shard for this rank: X ~ N(0,1), planted CP model, y / labels."""
     g = torch.Generator(device=dev).manual_seed(1234 + rank_id)
     N, dims, R = cfg["rows"], cfg["dims"], cfg["rank"]
-    X = torch.randn((N,) + tuple(dims), device=dev, generator=g, dtype=torch.float32)
+    if cfg.get("windowed"):
+        from tensor_regression_amd.util import windowed_view
+        L = dims[0]
+        Xu = torch.randn((N + L - 1,) + tuple(dims[1:]), device=dev, generator=g, dtype=torch.float32)
+        X, _ = windowed_view(Xu, torch.zeros(N + L - 1, device=dev), (0, L))
+    else:
+        X = torch.randn((N,) + tuple(dims), device=dev, generator=g, dtype=torch.float32)
     gc = torch.Generator().manual_seed(99)  # planted factors identical on every rank
     if cfg["kind"] == "spectral":
         from tensor_regression_amd.spectral_tensor_regression import lin_model as spec_lin
