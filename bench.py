@@ -234,7 +234,7 @@ def main():
     elif kt["stream_fused"][1]:
         dom = "stream_fused"
         bytes_launch = N * P * 4 + N * 4
-        dom_name = "k_linear_fused"
+        dom_name = "k_linear_cluster" if "cluster-1pass" in plan.describe else "k_linear_fused"
     else:
         dom = "stream_rows" if kt["stream_rows"][0] >= kt["stream_cols"][0] else "stream_cols"
         bytes_launch = N * P * 4 + N * 4 * (cfg.get("classes", 1))

@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define TR_ABI_VERSION 3
+#define TR_ABI_VERSION 4
 
 #define TR_MODEL_LINEAR 0      /* CP_linear_regression: y_hat = <X, [[w; Phi]]> + bias, MSE */
 #define TR_MODEL_MULTINOMIAL 1 /* CP_logistic_regression: softmax(<X, [[w; Phi]]>), CE(weight) */
@@ -104,6 +104,16 @@ const char* tr_plan_describe(const tr_plan* plan);
  * paths, and a misaligned X on a vector plan is rejected with TR_E_ARG.
  */
 int tr_plan_set_x_stride(tr_plan* plan, int64_t stride);
+
+/*
+ * Device status of the plan's kernels since the last call (synchronises the device).
+ * *status = 0: healthy.  Bit 0: a cross-workgroup exchange of the single-pass kernel for wide
+ * rows (P beyond one CU's LDS) gave up waiting for a partner workgroup — it happens only when
+ * the GPU is shared with another kernel so the cluster was not co-resident; that call's
+ * gradient and loss are NaN.  No reference counterpart (the reference has no device kernels);
+ * fit loops call it at their host synchronisation points and raise.
+ */
+int tr_plan_status(tr_plan* plan, int32_t* status);
 
 /*
  * Forward model only (predict path).

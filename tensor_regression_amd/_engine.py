@@ -174,6 +174,16 @@ class Plan:
         check(self.lib.tr_plan_read_timing(self.h, ms, cnt), "tr_plan_read_timing")
         return {k: (ms[i], cnt[i]) for i, k in enumerate(_lib.KERNEL_KINDS)}
 
+    def check_status(self):
+        """Raise if a kernel of this plan reported a device-side failure (tr_plan_status: a wide-row
+        cluster exchange that timed out because the GPU was shared).  Synchronises the device."""
+        torch.cuda.synchronize(self.dev)
+        st = ctypes.c_int32(0)
+        check(self.lib.tr_plan_status(self.h, ctypes.byref(st)), "tr_plan_status")
+        if st.value:
+            raise RuntimeError(f"gfx950 kernel status {st.value:#x}: a cross-workgroup exchange timed out "
+                               "(the GPU was shared with another kernel); the affected gradients are NaN")
+
     # ---- entry points ------------------------------------------------------------------------
     def _set_stride(self, X):
         """Tell the plan X's row stride (windowed / strided views) when it changes."""
@@ -380,6 +390,7 @@ def run_adam_fit(plan, X, target, class_weight, norm, arena, weights, lambda_L2,
             plan.adam_step(arena, grad, m, v, vmax, lambda_L2, hp, it + 1, hist, base, it, patience, tol, stop)
         ii += n
         stopped_at = int(stop.item())  # one host sync per chunk
+        plan.check_status()
         if verbose_cb is not None:
             verbose_cb.after_step(ii - 1, float(hist[base + ii - 1].item()))
         if stopped_at:

@@ -36,6 +36,12 @@ struct tr_plan {
   // single-pass linear strategy
   int fused = 0, fT = 0, fCH = 0, fgrid = 0;
   int mfma_rows = 0;  // multinomial forward on the matrix cores
+  // single-pass linear strategy for P beyond one CU's LDS (clusters of cS workgroups)
+  int cluster = 0, cCH = 0, cS = 0, cncl = 0;
+  unsigned long long* gran = nullptr;  // cluster exchange granules (2 row slots x S per cluster)
+  uint32_t* err_word = nullptr;        // device status word (bit 0: a cluster exchange timed out)
+  uint32_t cl_tag = 0;                 // last granule tag used (tags only grow; wrap -> re-zero)
+  int64_t gran_n = 0;
   // spectral model (TR_MODEL_SPECTRAL)
   SpecGeom sg{};
   float* Phi0 = nullptr;
@@ -158,6 +164,37 @@ static void choose_fused(tr_plan* p) {
   }
 }
 
+// Single pass for a linear P too wide for one CU's LDS: clusters of S workgroups split every row
+// into S feature slices (tr_cluster.hip).  Among the spill-free slice widths pick the one that
+// wastes the fewest lanes: P / (S * slice) for the padding of the last slice, times the
+// fraction of CUs the floor(ncu / S) clusters keep busy.
+static void choose_cluster(tr_plan* p) {
+  p->cluster = 0;
+  if (p->model != TR_MODEL_LINEAR || p->fused || p->P % 4 != 0 || p->xld % 4 != 0 || env_flag("TR_FORCE_TWOPASS") ||
+      env_flag("TR_NO_CLUSTER"))
+    return;
+  const char* force_ch = std::getenv("TR_CLUSTER_CH");  // experiment knob
+  double best = 0.0;
+  for (int k = 0; k < linear_cluster_num_ch(); ++k) {
+    const int CH = linear_cluster_ch(k);
+    if (force_ch != nullptr && std::atoi(force_ch) != CH) continue;
+    const int64_t PS = linear_cluster_slice(CH);
+    const int64_t S = (p->P + PS - 1) / PS;
+    if (S < 2 || S > 64 || S > p->ncu) continue;
+    int per_cu = 0;
+    if (prepare_linear_cluster(CH, &per_cu) != hipSuccess || per_cu < 1) continue;
+    const int64_t ncl = p->ncu / S;  // one workgroup per CU: every member co-resident
+    const double score = (double)p->P / (double)(S * PS) * (double)(ncl * S) / (double)p->ncu;
+    if (score > best + 1e-9) {
+      best = score;
+      p->cluster = 1;
+      p->cCH = CH;
+      p->cS = (int)S;
+      p->cncl = (int)ncl;
+    }
+  }
+}
+
 extern "C" int tr_plan_create(tr_plan** out, int device, int model, int n_feature_modes,
                               const int64_t* feature_dims, int n_classes, int rank, int64_t max_rows,
                               const int32_t* non_negative, float softplus_beta,
@@ -251,6 +288,7 @@ extern "C" int tr_plan_create(tr_plan** out, int device, int model, int n_featur
     p->ncu = ncu;
 
   choose_fused(p);
+  choose_cluster(p);
   p->mfma_rows = (model == TR_MODEL_MULTINOMIAL && rows_mfma_supported(C, P) && !env_flag("TR_NO_MFMA")) ? 1 : 0;
 
   // two-pass slab budget: max(16 MiB, 2 % of X bytes)
@@ -267,14 +305,18 @@ extern "C" int tr_plan_create(tr_plan** out, int device, int model, int n_featur
   if (p->fused && p->fgrid > p->gpart_slabs) p->gpart_slabs = p->fgrid;
   p->dpart_n = rows_num_waves(C, max_rows) + rows_mfma_num_waves(max_rows) + 64;
   if (p->fused && p->fgrid > p->dpart_n) p->dpart_n = p->fgrid;
+  if (p->cluster && p->cncl > p->gpart_slabs) p->gpart_slabs = p->cncl;
+  if (p->cluster && p->cncl > p->dpart_n) p->dpart_n = p->cncl;
+  p->gran_n = 2 * (int64_t)p->ncu;  // >= 2 slots x S x ncl for any cluster shape
 
   // workspace carve (256-B aligned pieces)
   auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
   // dense B / G: class-major; padded to 16 class rows for the MFMA forward (pad rows stay zero)
   const int64_t dense_rows = p->mfma_rows && C < 16 ? 16 : C;
   const size_t b_phi = al(fs.nfelem * 4), b_dense = al((size_t)dense_rows * P * 4), b_gpart = al((size_t)p->gpart_slabs * p->ncols * 4),
-               b_row = al((size_t)max_rows * C * 4), b_dpart = al((size_t)p->dpart_n * 2 * 8);
-  p->ws_bytes = 2 * b_phi + 2 * b_dense + b_gpart + b_row + b_dpart;
+               b_row = al((size_t)max_rows * C * 4), b_dpart = al((size_t)p->dpart_n * 2 * 8),
+               b_gran = al((size_t)p->gran_n * 8 + 16);
+  p->ws_bytes = 2 * b_phi + 2 * b_dense + b_gpart + b_row + b_dpart + b_gran;
   e = hipMalloc(&p->ws, p->ws_bytes);
   if (e != hipSuccess) {
     delete p;
@@ -294,6 +336,9 @@ extern "C" int tr_plan_create(tr_plan** out, int device, int model, int n_featur
   p->rowbuf = (float*)c;
   c += b_row;
   p->dpart = (double*)c;
+  c += b_dpart;
+  p->gran = (unsigned long long*)c;
+  p->err_word = (uint32_t*)(c + p->gran_n * 8);
   TR_HIP(hipMemset(p->ws, 0, p->ws_bytes));
 
   char buf[512];
@@ -301,9 +346,14 @@ extern "C" int tr_plan_create(tr_plan** out, int device, int model, int n_featur
                 "model=%s K=%d C=%d R=%d P=%lld nparams=%lld ncu=%d path=%s%s T=%d CH=%d grid=%d W=%d "
                 "max_slabs=%lld workspace=%.1fMiB",
                 model == TR_MODEL_LINEAR ? "linear" : "multinomial", p->K, C, rank, (long long)P,
-                (long long)p->nparams, p->ncu, p->fused ? "fused-1pass" : "2pass", p->mfma_rows ? "+mfma-fwd" : "", p->fT,
-                p->fCH, p->fgrid,
-                p->W, (long long)p->max_slabs, p->ws_bytes / 1048576.0);
+                (long long)p->nparams, p->ncu, p->fused ? "fused-1pass" : (p->cluster ? "cluster-1pass" : "2pass"),
+                p->mfma_rows ? "+mfma-fwd" : "", p->cluster ? 512 : p->fT, p->cluster ? p->cCH : p->fCH,
+                p->cluster ? p->cS * p->cncl : p->fgrid, p->W, (long long)p->max_slabs, p->ws_bytes / 1048576.0);
+  if (p->cluster) {
+    char b2[96];
+    std::snprintf(b2, sizeof(b2), " S=%d clusters=%d", p->cS, p->cncl);
+    std::strncat(buf, b2, sizeof(buf) - std::strlen(buf) - 1);
+  }
   p->desc = buf;
   *out = p;
   return 0;
@@ -435,6 +485,10 @@ extern "C" int tr_plan_set_x_stride(tr_plan* p, int64_t stride) {
     p->fused = had_fused;
     p->fgrid = fgrid;
   }
+  const int had_cluster = p->cluster;
+  const int cncl = p->cncl;
+  choose_cluster(p);
+  if (p->cluster && (!had_cluster || p->cncl > cncl)) p->cluster = 0;  // keep within the workspace
   p->mfma_rows = (p->model == TR_MODEL_MULTINOMIAL && rows_mfma_supported(p->C, p->P) && x % 4 == 0 &&
                   !env_flag("TR_NO_MFMA"))
                      ? 1
@@ -593,6 +647,28 @@ extern "C" int tr_loss_grad(tr_plan* p, const float* X, int64_t n_rows, const vo
       TR_HIP(launch_reduce_slabs(4, p->gpart, p->fgrid, p->P, p->G, p->dpart, p->fgrid, 1.0 / norm, loss_slot,
                                  bias_slot, stop_flag, st));
     }
+  } else if (p->cluster) {
+    if (yhat_out != nullptr)
+      TR_HIP(launch_rows(1, MODE_LIN_PRED, p->W, X, N, p->P, p->xld, p->dense, bias, nullptr, nullptr, 0.f, yhat_out,
+                         nullptr, nullptr, stop_flag, st));
+    const int64_t rpc = (N + p->cncl - 1) / p->cncl;
+    if ((uint64_t)p->cl_tag + (uint64_t)rpc + 2 >= 0xFFFFFFFFull) {  // tags would wrap: start over
+      TR_HIP(hipMemsetAsync(p->gran, 0, (size_t)p->gran_n * 8, st));
+      p->cl_tag = 0;
+    }
+    const uint32_t tag0 = p->cl_tag + 1;
+    p->cl_tag += (uint32_t)rpc + 1;
+    {
+      TimedLaunch tl(p, st, TR_KERNEL_STREAM_FUSED);
+      TR_HIP(launch_linear_cluster(p->cCH, p->cS, p->cncl, X, N, p->P, p->xld, p->dense, bias, (const float*)target,
+                                   (float)(2.0 / norm), p->gpart, p->dpart, rpc, reverse, tag0, p->gran, p->err_word,
+                                   stop_flag, st));
+    }
+    {
+      TimedLaunch tl(p, st, TR_KERNEL_REDUCE);
+      TR_HIP(launch_reduce_slabs(4, p->gpart, p->cncl, p->P, p->G, p->dpart, p->cncl, 1.0 / norm, loss_slot,
+                                 bias_slot, stop_flag, st));
+    }
   } else {
     const int C = p->C;
     TimedLaunch* tl_rows = new TimedLaunch(p, st, TR_KERNEL_STREAM_ROWS);
@@ -688,6 +764,18 @@ extern "C" int tr_adam_step(tr_plan* p, float* params, const float* grad, float*
   TimedLaunch tl(p, (hipStream_t)stream, TR_KERNEL_UPDATE);
   TR_HIP(launch_update(p->fs, p->has_bias, params, grad, ua, exp_avg, exp_avg_sq, max_exp_avg_sq, nullptr, nullptr,
                        loss_hist, stop_flag, (hipStream_t)stream));
+  return 0;
+}
+
+extern "C" int tr_plan_status(tr_plan* p, int32_t* status) {
+  if (p == nullptr || status == nullptr) return fail(TR_E_ARG, "NULL argument");
+  *status = 0;
+  if (p->err_word == nullptr) return 0;
+  TR_HIP(hipSetDevice(p->device));
+  uint32_t w = 0;
+  TR_HIP(hipMemcpy(&w, p->err_word, 4, hipMemcpyDeviceToHost));  // synchronises the device
+  if (w != 0) TR_HIP(hipMemset(p->err_word, 0, 4));
+  *status = (int32_t)w;
   return 0;
 }
 

@@ -45,6 +45,17 @@ hipError_t launch_linear_fused(int T, int CH, int grid, const float* X, int64_t 
                                float* gpart, double* dpart, float* yhat, int64_t rows_per_wg,
                                int reverse, const int32_t* stop, hipStream_t st);
 hipError_t prepare_linear_fused(int T, int CH, size_t lds_bytes, int* wg_per_cu);
+// single pass for P beyond one CU's LDS (tr_cluster.hip): clusters of S workgroups, member s
+// owning feature slice [s*slice(CH), (s+1)*slice(CH)), exchanging per-row partial dots
+int linear_cluster_num_ch(void);
+int linear_cluster_ch(int k);
+int64_t linear_cluster_slice(int CH);
+size_t linear_cluster_lds(int CH);
+hipError_t prepare_linear_cluster(int CH, int* wg_per_cu);
+hipError_t launch_linear_cluster(int CH, int S, int ncl, const float* X, int64_t N, int64_t P, int64_t xld,
+                                 const float* B, const float* bias, const float* y, float scale, float* gpart,
+                                 double* dpart, int64_t rows_per_cl, int reverse, uint32_t tag0,
+                                 unsigned long long* gran, uint32_t* err, const int32_t* stop, hipStream_t st);
 int rows_rb(int C);
 int cols_cw(int C);
 bool rows_supported(int C);

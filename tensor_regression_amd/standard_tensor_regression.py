@@ -256,6 +256,7 @@ class CP_linear_regression():
                     convergence_reached = True
                     break
             optimizer.step(closure)
+        plan.check_status()
         if (verbose is True) or (verbose >= 1):
             print('Convergence reached' if convergence_reached else
                   'Reached maximum number of iterations without convergence')

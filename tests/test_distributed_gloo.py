@@ -34,6 +34,9 @@ class OraclePlan:
         self.num_grads = self.num_params + 1
         self.device_str = "cpu"
 
+    def check_status(self):
+        pass
+
     def factors(self, arena):
         return [arena[self.offsets[f]:self.offsets[f + 1]].view(s).clone() for f, s in enumerate(self.shapes)]
 

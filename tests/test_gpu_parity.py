@@ -222,7 +222,10 @@ LIN_SHAPES = [
     ((300, 256, 128), 8),      # config-2 row width (fused T=1024 CH=8)
     ((257, 6, 7, 8, 3), 5),    # 4 feature modes, unaligned
     ((64, 10, 10), 33),        # rank > 32 (RMAX 64 MTTKRP)
-    ((129, 100, 101), 2),      # P > LDS: two-pass only
+    ((129, 100, 101), 2),      # P % 16 != 0 for every fused T: two-pass only
+    ((300, 64, 64, 32), 16),   # config-4 row (P = 131072 > LDS): cluster single pass, 5 slices
+    ((77, 45000), 3),          # one wide mode: 2-slice cluster, ragged last slice
+    ((2, 200, 332), 4),        # N < number of clusters: most clusters own no rows
 ]
 
 
@@ -299,12 +302,14 @@ def _multinomial_sweep(shape, C, rank):
     np.testing.assert_allclose(S.cpu().numpy(), ref["probs"], rtol=RTOL, atol=1e-6)
 
 
-def test_bitwise_reproducible():
-    """Fixed-order reductions: two runs give bit-identical factors."""
+@pytest.mark.parametrize("shape", [(3000, 64, 32), (700, 64, 64, 32)])
+def test_bitwise_reproducible(shape):
+    """Fixed-order reductions: two runs give bit-identical factors (single-pass path and the
+    cluster single pass, whose cross-workgroup partial dots are summed in slice order)."""
     from tensor_regression_amd import CP_linear_regression
     g = torch.Generator().manual_seed(5)
-    X = torch.randn(3000, 64, 32, generator=g).to(DEV)
-    y = torch.randn(3000, generator=g).to(DEV)
+    X = torch.randn(*shape, generator=g).to(DEV)
+    y = torch.randn(shape[0], generator=g).to(DEV)
     outs = []
     for _ in range(2):
         torch.manual_seed(3)
@@ -314,6 +319,21 @@ def test_bitwise_reproducible():
     assert outs[0][1] == outs[1][1]
     for a, b in zip(outs[0][0], outs[1][0]):
         assert np.array_equal(a, b)
+
+
+def test_cluster_path_selected_for_wide_rows():
+    """Rows wider than one CU's LDS (config 4) take the cluster single pass, and a fit through it
+    reports a healthy device status (no exchange timed out)."""
+    from tensor_regression_amd import CP_linear_regression
+    from tensor_regression_amd import standard_tensor_regression as S
+    S._plan_cache.clear()
+    X = torch.randn(512, 64, 64, 32, device=DEV)
+    y = torch.randn(512, device=DEV)
+    m = CP_linear_regression(X.shape, rank=16, device=DEV)
+    m.fit_Adam(X, y, lambda_L2=0.01, max_iter=3, tol=0, patience=10, Adam_kwargs={"lr": 0.01})
+    assert "cluster-1pass" in m._plan.describe and "S=5" in m._plan.describe, m._plan.describe
+    m._plan.check_status()
+    assert np.all(np.isfinite(m.loss_running))
 
 
 def test_sharded_sum_equals_full():

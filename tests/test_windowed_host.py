@@ -53,15 +53,18 @@ DEV = "cuda:0"
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("twopass", [False, True])
-def test_windowed_linear_fit_equals_materialised(twopass, monkeypatch):
+@pytest.mark.parametrize("twopass,F", [(False, 32), (True, 32), (False, 4096)])
+def test_windowed_linear_fit_equals_materialised(twopass, F, monkeypatch):
+    """F = 32: windows of 16 rows -> P = 512 (single pass); F = 4096: P = 65536 > LDS (cluster
+    single pass reading the overlapping windows through the row stride)."""
     from tensor_regression_amd import standard_tensor_regression as S
     if twopass:
         monkeypatch.setenv("TR_FORCE_TWOPASS", "1")
     S._plan_cache.clear()
     g = torch.Generator().manual_seed(1)
-    X = torch.randn(3000, 32, generator=g).to(DEV)  # untiled (T, F): windows of 16 rows -> P = 512
-    y = torch.randn(3000, generator=g).to(DEV)
+    T = 3000 if F == 32 else 400
+    X = torch.randn(T, F, generator=g).to(DEV)  # untiled (T, F)
+    y = torch.randn(T, generator=g).to(DEV)
     Xw, yw = util.windowed_view(X, y, (-8, 8))
     Xm = Xw.contiguous()
     res = []
@@ -70,6 +73,8 @@ def test_windowed_linear_fit_equals_materialised(twopass, monkeypatch):
         m = S.CP_linear_regression(XX.shape, rank=4, device=DEV)
         m.fit_Adam(XX, yw, lambda_L2=0.01, max_iter=20, tol=0, patience=10, Adam_kwargs={"lr": 0.01})
         res.append((m.loss_running, [a.detach().cpu() for a in m.Bcp], m._plan.describe))
+    if F == 4096:
+        assert "cluster-1pass" in res[0][2], res[0][2]
     assert res[0][0] == res[1][0], "windowed view must give the materialised result bit for bit"
     for a, b in zip(res[0][1], res[1][1]):
         assert torch.equal(a, b)
