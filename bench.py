@@ -231,6 +231,10 @@ def main():
         # fwd GEMM X_n^T Phi0 + bwd GEMM X_n dT_n: 2 * 2*W*D*K flops per sample
         flops_launch = 4 * N * P * (R + cfg["rank_spectral"] * (cfg["n_complex_dim"] + 1))
         dom_name = "k_spec_fused"
+    elif kt["stream_fused"][1] and "mnl-fused-1pass" in plan.describe:
+        dom = "stream_fused"
+        bytes_launch = N * P * 4 + N * 8  # X row + int64 label per sample
+        dom_name = "k_mnl_fused"
     elif kt["stream_fused"][1]:
         dom = "stream_fused"
         bytes_launch = N * P * 4 + N * 4

@@ -16,6 +16,7 @@
 
 #include "../../include/tensor_regression_hip.h"
 #include "tr_kernels.h"
+#include "tr_mnl.h"
 #include "tr_spectral.h"
 
 using namespace tr;
@@ -42,6 +43,9 @@ struct tr_plan {
   uint32_t* err_word = nullptr;        // device status word (bit 0: a cluster exchange timed out)
   uint32_t cl_tag = 0;                 // last granule tag used (tags only grow; wrap -> re-zero)
   int64_t gran_n = 0;
+  // single-pass factored multinomial strategy (two feature modes, tr_mnl.hip)
+  int mnl = 0;
+  MnlGeom mg{};
   // spectral model (TR_MODEL_SPECTRAL)
   SpecGeom sg{};
   float* Phi0 = nullptr;
@@ -195,6 +199,21 @@ static void choose_cluster(tr_plan* p) {
   }
 }
 
+// Single pass for the multinomial model with two feature modes: the factored kernel contracts X
+// with Phi0 / Phi1 directly (no dense B) and reads every X row once (tr_mnl.hip).
+static void choose_mnl(tr_plan* p) {
+  p->mnl = 0;
+  if (p->model != TR_MODEL_MULTINOMIAL || p->K != 2 || p->xld % 4 != 0 || env_flag("TR_FORCE_TWOPASS") ||
+      env_flag("TR_NO_MNL_FUSED"))
+    return;
+  MnlGeom g;
+  if (!mnl_geom_init(&g, p->fs.dim[0], p->fs.dim[1], p->R, p->C, nullptr)) return;
+  int ok = 0;
+  if (mnl_prepare(g, &ok) != hipSuccess || !ok) return;
+  p->mg = g;
+  p->mnl = 1;
+}
+
 extern "C" int tr_plan_create(tr_plan** out, int device, int model, int n_feature_modes,
                               const int64_t* feature_dims, int n_classes, int rank, int64_t max_rows,
                               const int32_t* non_negative, float softplus_beta,
@@ -289,6 +308,7 @@ extern "C" int tr_plan_create(tr_plan** out, int device, int model, int n_featur
 
   choose_fused(p);
   choose_cluster(p);
+  choose_mnl(p);
   p->mfma_rows = (model == TR_MODEL_MULTINOMIAL && rows_mfma_supported(C, P) && !env_flag("TR_NO_MFMA")) ? 1 : 0;
 
   // two-pass slab budget: max(16 MiB, 2 % of X bytes)
@@ -307,13 +327,19 @@ extern "C" int tr_plan_create(tr_plan** out, int device, int model, int n_featur
   if (p->fused && p->fgrid > p->dpart_n) p->dpart_n = p->fgrid;
   if (p->cluster && p->cncl > p->gpart_slabs) p->gpart_slabs = p->cncl;
   if (p->cluster && p->cncl > p->dpart_n) p->dpart_n = p->cncl;
+  if (p->mnl && p->ncu > p->dpart_n) p->dpart_n = p->ncu;
   p->gran_n = 2 * (int64_t)p->ncu;  // >= 2 slots x S x ncl for any cluster shape
 
   // workspace carve (256-B aligned pieces)
   auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
   // dense B / G: class-major; padded to 16 class rows for the MFMA forward (pad rows stay zero)
   const int64_t dense_rows = p->mfma_rows && C < 16 ? 16 : C;
-  const size_t b_phi = al(fs.nfelem * 4), b_dense = al((size_t)dense_rows * P * 4), b_gpart = al((size_t)p->gpart_slabs * p->ncols * 4),
+  size_t b_gpart = al((size_t)p->gpart_slabs * p->ncols * 4), b_dense = al((size_t)dense_rows * P * 4);
+  if (p->mnl) {  // one arena-layout slab per CU; G holds the reduced arena
+    if (b_gpart < al((size_t)p->ncu * p->mg.slab * 4)) b_gpart = al((size_t)p->ncu * p->mg.slab * 4);
+    if (b_dense < al((size_t)p->mg.slab * 4)) b_dense = al((size_t)p->mg.slab * 4);
+  }
+  const size_t b_phi = al(fs.nfelem * 4),
                b_row = al((size_t)max_rows * C * 4), b_dpart = al((size_t)p->dpart_n * 2 * 8),
                b_gran = al((size_t)p->gran_n * 8 + 16);
   p->ws_bytes = 2 * b_phi + 2 * b_dense + b_gpart + b_row + b_dpart + b_gran;
@@ -346,12 +372,19 @@ extern "C" int tr_plan_create(tr_plan** out, int device, int model, int n_featur
                 "model=%s K=%d C=%d R=%d P=%lld nparams=%lld ncu=%d path=%s%s T=%d CH=%d grid=%d W=%d "
                 "max_slabs=%lld workspace=%.1fMiB",
                 model == TR_MODEL_LINEAR ? "linear" : "multinomial", p->K, C, rank, (long long)P,
-                (long long)p->nparams, p->ncu, p->fused ? "fused-1pass" : (p->cluster ? "cluster-1pass" : "2pass"),
+                (long long)p->nparams, p->ncu,
+                p->fused ? "fused-1pass" : (p->cluster ? "cluster-1pass" : (p->mnl ? "mnl-fused-1pass" : "2pass")),
                 p->mfma_rows ? "+mfma-fwd" : "", p->cluster ? 512 : p->fT, p->cluster ? p->cCH : p->fCH,
                 p->cluster ? p->cS * p->cncl : p->fgrid, p->W, (long long)p->max_slabs, p->ws_bytes / 1048576.0);
   if (p->cluster) {
     char b2[96];
     std::snprintf(b2, sizeof(b2), " S=%d clusters=%d", p->cS, p->cncl);
+    std::strncat(buf, b2, sizeof(buf) - std::strlen(buf) - 1);
+  }
+  if (p->mnl) {
+    char b2[128];
+    std::snprintf(b2, sizeof(b2), " units=%d nbuf=%d lds=%.1fKiB", p->mg.nunits, p->mg.nbuf,
+                  p->mg.lds_floats * 4 / 1024.0);
     std::strncat(buf, b2, sizeof(buf) - std::strlen(buf) - 1);
   }
   p->desc = buf;
@@ -489,6 +522,9 @@ extern "C" int tr_plan_set_x_stride(tr_plan* p, int64_t stride) {
   const int cncl = p->cncl;
   choose_cluster(p);
   if (p->cluster && (!had_cluster || p->cncl > cncl)) p->cluster = 0;  // keep within the workspace
+  const int had_mnl = p->mnl;
+  choose_mnl(p);
+  if (p->mnl && !had_mnl) p->mnl = 0;  // keep within the workspace
   p->mfma_rows = (p->model == TR_MODEL_MULTINOMIAL && rows_mfma_supported(p->C, p->P) && x % 4 == 0 &&
                   !env_flag("TR_NO_MFMA"))
                      ? 1
@@ -498,7 +534,7 @@ extern "C" int tr_plan_set_x_stride(tr_plan* p, int64_t stride) {
 
 static bool x_vec_paths(const tr_plan* p) {
   if (p->model == TR_MODEL_SPECTRAL) return p->sg.vec != 0;
-  return p->W == 4 || p->fused || p->mfma_rows;
+  return p->W == 4 || p->fused || p->mfma_rows || p->mnl;
 }
 static int check_x_align(const tr_plan* p, const float* X) {
   if (X != nullptr && x_vec_paths(p) && (reinterpret_cast<uintptr_t>(X) & 15u) != 0)
@@ -621,6 +657,29 @@ extern "C" int tr_loss_grad(tr_plan* p, const float* X, int64_t n_rows, const vo
     }
     TimedLaunch tl(p, st, TR_KERNEL_MTTKRP);
     TR_HIP(launch_spec_chain(p->nparams, p->G, p->dphi, grad_out, stop_flag, st));
+    return 0;
+  }
+  if (p->mnl) {
+    const int reverse = (int)(p->parity & 1u);
+    p->parity++;
+    {
+      TimedLaunch tl(p, st, TR_KERNEL_PREP);
+      TR_HIP(launch_prep_factors(p->fs, params, p->sp_beta, p->sp_thr, p->phi, p->dphi, stop_flag, st));
+    }
+    const int grid = p->ncu;
+    const int64_t rpw = (n_rows + grid - 1) / grid;
+    {
+      TimedLaunch tl(p, st, TR_KERNEL_STREAM_FUSED);
+      TR_HIP(launch_mnl_fused(p->mg, grid, X, n_rows, p->xld, p->phi, weights, (const int64_t*)target, class_weight,
+                              (float)(1.0 / norm), p->gpart, p->dpart, rpw, reverse, stop_flag, st));
+    }
+    {
+      TimedLaunch tl(p, st, TR_KERNEL_REDUCE);
+      TR_HIP(launch_reduce_slabs(4, p->gpart, grid, p->mg.slab, p->G, p->dpart, grid, 1.0 / norm,
+                                 grad_out + p->nparams, nullptr, stop_flag, st));
+    }
+    TimedLaunch tl(p, st, TR_KERNEL_MTTKRP);
+    TR_HIP(launch_spec_chain(p->fs.nfelem, p->G, p->dphi, grad_out, stop_flag, st));
     return 0;
   }
   int rc = factor_prep(p, params, weights, stop_flag, st);

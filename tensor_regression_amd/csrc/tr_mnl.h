@@ -1,0 +1,52 @@
+// tr_mnl.h — host/device interface of the factored single-pass multinomial kernel
+// (multinomial_tensor_regression.py: model 148-187, the CrossEntropyLoss of fit_Adam 448-457).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+namespace tr {
+
+constexpr int kMnlRMax = 32;  // rank bound of the factored kernel (8 rank blocks of 4)
+constexpr int kMnlCMax = 16;  // classes: one 16-lane DPP row
+constexpr int kMnlGMax = 8;   // LDS-DMA instructions per wave per sample (sample <= 64 KiB)
+
+// Geometry of one multinomial model with two feature modes, X (N, I, J), factors
+// Phi0 (I x R), Phi1 (J x R), PhiC (C x R), passed to the kernel by value.
+//
+// Per sample the kernel never forms the dense (I*J x C) coefficient tensor: it contracts X_n
+// with the two feature factors directly,
+//     T[i, r] = sum_j X_n[i, j] Phi1[j, r]      (A-units)
+//     V[j, r] = sum_i X_n[i, j] Phi0[i, r]      (B-units)
+// on v_mfma_f32_4x4x1_16b_f32 (16 blocks of 4x4 outer products: 4 ranks per instruction, no
+// padding of R to 16).  A unit is a (64 output rows) x (64-deep k range) x (4 ranks) tile of
+// one of the two GEMMs; each wave owns upw <= 2 units and keeps their B operands (64 factor
+// values per lane) in registers for the whole launch.
+struct MnlGeom {
+  int I, J, R, C;
+  int JQ;         // 16-B chunks per X row (J / 4)
+  int smask;      // XOR swizzle of the chunk index in LDS (row i: chunk q stored at q ^ (i & smask))
+  int nchunk;     // 16-B chunks per sample (I * J / 4)
+  int nbuf;       // LDS ring depth (samples)
+  int nib, njb, nrb, Rp;  // 64-row blocks of I and J, rank blocks of 4, Rp = 4 * nrb
+  int nA, nunits, upw, nsets;  // A-units, all units (2 nA, one per wave), units per wave (1), nib * njb
+  int full;       // I % 64 == 0 && J % 64 == 0 (no k-range guards)
+  int64_t offP1, offPC, nfelem, slab;  // arena offsets (floats); slab stride (nfelem rounded to 4)
+  // LDS carve (floats)
+  int oZ, oG, lds_floats;  // oZ: [2][16][4] Z partials; oG: LDS image of the arena (aliases the drained ring)
+};
+
+// Fills g; false (with a reason) when the shape is outside the kernel's envelope.
+bool mnl_geom_init(MnlGeom* g, int64_t I, int64_t J, int R, int C, std::string* why);
+// Sets the dynamic-LDS limit and checks the instantiation is spill-free and fits a CU.
+hipError_t mnl_prepare(const MnlGeom& g, int* ok);
+// One workgroup per CU over a contiguous sample range (reversed when `reverse`).  Writes one
+// phi-space gradient slab per workgroup in arena layout [dPhi0 | dPhi1 | dPhiC] (stride g.slab)
+// and (sum_n cw[y_n] * CE_n, 0) into dpart[2 * wg].
+hipError_t launch_mnl_fused(const MnlGeom& g, int grid, const float* X, int64_t N, int64_t xld, const float* phi,
+                            const float* w, const int64_t* lab, const float* class_w, float scale, float* gpart,
+                            double* dpart, int64_t rows_per_wg, int reverse, const int32_t* stop, hipStream_t st);
+
+}  // namespace tr

@@ -32,7 +32,8 @@ RTOL = 1e-5
 @contextlib.contextmanager
 def path(kind):
     """kind: 'auto' (plan's choice: single pass / MFMA forward where eligible), 'twopass'
-    (linear: force the two-pass kernels) or 'valu' (multinomial: force the VALU forward)."""
+    (force the two-pass kernels: linear rows/cols, multinomial MFMA forward + cols) or 'valu'
+    (multinomial: two-pass with the VALU forward)."""
     from tensor_regression_amd import standard_tensor_regression as S
     saved = {k: os.environ.get(k) for k in ("TR_FORCE_TWOPASS", "TR_NO_MFMA")}
     for k in saved:
@@ -40,6 +41,7 @@ def path(kind):
     if kind == "twopass":
         os.environ["TR_FORCE_TWOPASS"] = "1"
     if kind == "valu":
+        os.environ["TR_FORCE_TWOPASS"] = "1"
         os.environ["TR_NO_MFMA"] = "1"
     S._plan_cache.clear()
     try:
@@ -137,7 +139,7 @@ def test_linear_golden(name, kind):
             _assert_factors(model.Bcp, d["Bcp_final2_list"])
 
 
-@pytest.mark.parametrize("kind", ["auto", "valu"])
+@pytest.mark.parametrize("kind", ["auto", "twopass", "valu"])
 @pytest.mark.parametrize("name", MNL)
 def test_multinomial_golden(name, kind):
     with path(kind):
@@ -263,10 +265,14 @@ def test_linear_sweep_vs_oracle(shape, rank, kind):
 
 
 MNL_SHAPES = [((50, 8, 4), 2, 2), ((200, 16, 8), 10, 4), ((97, 5, 7), 16, 3), ((64, 33), 3, 1),
-              ((128, 4, 4, 4), 5, 6), ((333, 32, 32), 10, 8), ((40, 64), 16, 2), ((3, 32), 3, 2)]
+              ((128, 4, 4, 4), 5, 6), ((333, 32, 32), 10, 8), ((40, 64), 16, 2), ((3, 32), 3, 2),
+              # factored single pass: ragged 64-blocks, R % 4 != 0, k ranges split over 2 blocks,
+              # fewer samples than workgroups, the config-3 sample shape, one class
+              ((300, 100, 12), 7, 5), ((257, 64, 128), 4, 8), ((100, 128, 64), 10, 8), ((700, 72, 40), 3, 3),
+              ((90, 8, 8), 1, 2)]
 
 
-@pytest.mark.parametrize("kind", ["auto", "valu"])
+@pytest.mark.parametrize("kind", ["auto", "twopass", "valu"])
 @pytest.mark.parametrize("shape,C,rank", MNL_SHAPES)
 def test_multinomial_sweep_vs_oracle(shape, C, rank, kind):
     with path(kind):
@@ -281,7 +287,10 @@ def _multinomial_sweep(shape, C, rank):
     y = torch.randint(0, C, (shape[0],), generator=g)
     y[:C] = torch.arange(C)
     nn = [bool(i % 2 == 0) for i in range(len(shape))]
-    Bcp0 = [torch.randn(d, rank, generator=g) * 0.3 for d in list(shape[1:]) + [C]]
+    # keep the logits O(1) for wide rows (fp32 reduction-order noise grows with |Z|)
+    P = int(np.prod(shape[1:]))
+    sc = 0.3 * min(1.0, (2048.0 / P) ** (1.0 / len(shape)))
+    Bcp0 = [torch.randn(d, rank, generator=g) * sc for d in list(shape[1:]) + [C]]
     cw = (torch.rand(C, generator=g) + 0.5).numpy()
     lam = 0.02
     ref = cp_oracle.mnl_loss_grad(X, y, Bcp0, np.ones(rank), nn, cw, lam)
@@ -316,6 +325,29 @@ def test_bitwise_reproducible(shape):
         m = CP_linear_regression(X.shape, rank=4, device=DEV)
         m.fit_Adam(X, y, lambda_L2=0.01, max_iter=20, tol=0, patience=10, Adam_kwargs={"lr": 0.01})
         outs.append(([a.detach().cpu().numpy() for a in m.Bcp], list(m.loss_running)))
+    assert outs[0][1] == outs[1][1]
+    for a, b in zip(outs[0][0], outs[1][0]):
+        assert np.array_equal(a, b)
+
+
+def test_mnl_fused_path_selected_and_reproducible():
+    """Multinomial models with two feature modes take the factored single pass (config 3's
+    shape), and two fits give bit-identical factors (fixed-order unit and slab reductions)."""
+    from tensor_regression_amd import CP_logistic_regression
+    from tensor_regression_amd import standard_tensor_regression as S
+    S._plan_cache.clear()
+    g = torch.Generator().manual_seed(11)
+    X = torch.randn(2000, 128, 64, generator=g)
+    y = torch.randint(0, 10, (2000,), generator=g)
+    y[:10] = torch.arange(10)
+    outs = []
+    for _ in range(2):
+        torch.manual_seed(4)
+        mm = CP_logistic_regression(X.numpy(), y.numpy(), rank=8, device=DEV)
+        mm.fit_Adam(lambda_L2=0.01, max_iter=15, tol=0, patience=10, weights=np.ones(10),
+                    Adam_kwargs={"lr": 0.01})
+        assert "mnl-fused-1pass" in mm._plan.describe, mm._plan.describe
+        outs.append(([a.detach().cpu().numpy() for a in mm.Bcp], list(mm.loss_running)))
     assert outs[0][1] == outs[1][1]
     for a, b in zip(outs[0][0], outs[1][0]):
         assert np.array_equal(a, b)

@@ -1,0 +1,43 @@
+#!/usr/bin/env python3
+"""Per-phase cycle breakdown of the factored multinomial kernel (profiling build, GPU box).
+
+    make -C tensor_regression_amd/csrc prof-mnl
+    TR_HIP_LIB=$PWD/tensor_regression_amd/libtr_hip_mnlprof.so python tools/mnl_profile.py
+
+Phases per wave (__builtin_readcyclecounter deltas, averaged over workgroups, per sample):
+DMA wait, barrier, DMA issue, epilogue, GEMM, U partial.
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from tensor_regression_amd import _lib  # noqa: E402
+from tensor_regression_amd import CP_logistic_regression  # noqa: E402
+
+N, I, J, C, R = int(os.environ.get("N", 65536)), 128, 64, 10, 8
+dev = "cuda:0"
+g = torch.Generator(device=dev).manual_seed(0)
+X = torch.randn(N, I, J, device=dev, generator=g)
+y = torch.randint(0, C, (N,), device=dev, generator=g)
+y[:C] = torch.arange(C, device=dev)
+torch.manual_seed(1)
+m = CP_logistic_regression(X, y, rank=R, device=dev)
+m.fit_Adam(lambda_L2=0.01, max_iter=3, tol=0, patience=10, weights=np.ones(C), Adam_kwargs={"lr": 0.01})
+torch.cuda.synchronize()
+print(m._plan.describe)
+lib = _lib.load()
+fn = lib.tr_mnl_profile_read
+fn.restype = ctypes.c_int
+buf = (ctypes.c_ulonglong * (256 * 8 * 8))()
+assert fn(buf) == 0
+a = np.array(buf[:], dtype=np.float64).reshape(256, 8, 8)
+per_wg = (N + 255) // 256
+names = ["DMA wait", "barrier", "DMA issue", "epilogue", "GEMM", "U partial"]
+print("cycles/sample  " + " ".join(f"{n:>10s}" for n in names) + "      total")
+for w in range(8):
+    v = a[:, w, :6].mean(axis=0) / per_wg
+    print(f"wave {w}        " + " ".join(f"{x:10.0f}" for x in v) + f" {v.sum():10.0f}")

@@ -13,7 +13,7 @@ cd /tmp || exit 1
 for cfg in "$@"; do
   case $cfg in
     c2) alg=8590196736; dom=k_linear_fused ;;
-    c3) alg=2150105088; dom=k_rows_mfma ;;
+    c3) alg=2148007936; dom=k_mnl_fused ;;
     c4) alg=8590000128; dom=k_linear_cluster ;;
     c5) alg=4328783872; dom=k_spec_fused ;;
     *) alg=""; dom=k_linear_fused ;;
