@@ -33,9 +33,10 @@ struct MnlGeom {
   int nib, njb, nrb, Rp;  // 64-row blocks of I and J, rank blocks of 4, Rp = 4 * nrb
   int nA, nunits, upw, nsets;  // A-units, all units (2 nA, one per wave), units per wave (1), nib * njb
   int full;       // I % 64 == 0 && J % 64 == 0 (no k-range guards)
+  int spi;        // samples per barrier (2 when the ring holds >= 2 pairs)
   int64_t offP1, offPC, nfelem, slab;  // arena offsets (floats); slab stride (nfelem rounded to 4)
   // LDS carve (floats)
-  int oZ, oG, lds_floats;  // oZ: [2][16][4] Z partials; oG: LDS image of the arena (aliases the drained ring)
+  int oZ, oG, lds_floats;  // oZ: [2][2][16][4] Z partials; oG: LDS image of the arena (aliases the drained ring)
 };
 
 // Fills g; false (with a reason) when the shape is outside the kernel's envelope.

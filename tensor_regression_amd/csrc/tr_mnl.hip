@@ -28,12 +28,22 @@
 //   * End: units add their accumulators into an LDS image of the arena in fixed unit order;
 //     the workgroup writes one phi-space slab (k_reduce_slabs sums the slabs in index order,
 //     k_spec_chain applies softplus').  No float atomics: runs are bitwise reproducible.
+#include <cstdlib>
 #include <cstring>
 
 #include "tr_common.h"
 #include "tr_mnl.h"
 
 
+#ifndef TR_MNL_PRELOAD
+#define TR_MNL_PRELOAD 1  // read a sample's 16 X pieces of a unit into registers before its MFMAs
+#endif
+#ifndef TR_MNL_DMA_IN_GEMM
+#define TR_MNL_DMA_IN_GEMM 0  // issue the ring refill between GEMM steps instead of after the barrier
+#endif
+#ifndef TR_MNL_SPLIT
+#define TR_MNL_SPLIT 1  // B-waves run GEMM before the epilogue (SIMD partners pair matrix / vector work)
+#endif
 #ifndef TR_MNL_PROFILE
 #define TR_MNL_PROFILE 0  // profiling build only: per-phase cycle counts of every wave of WG 0..255
 #endif
@@ -101,10 +111,11 @@ __device__ __forceinline__ void mn_barrier() {
 // (mn_wait_vm) + barrier before a slot is read, barrier before a slot is refilled.
 __device__ __forceinline__ void mn_dma16(const float* gsrc, const float* lds_dst) {
   const uint32_t a = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) float*)lds_dst);
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"  // m0 is reserved, but this asm must own it
-  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off nt" ::"v"(gsrc), "s"(a) : "m0");
-#pragma clang diagnostic pop
+  uint32_t keep;  // m0 is compiler-reserved: save and restore it inside the statement
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(a)
+               : "memory");
 }
 // s_waitcnt vmcnt(n) for a wave-uniform runtime n (stricter than asked above 31: still safe)
 __device__ __forceinline__ void mn_wait_vm(int n) {
@@ -154,13 +165,14 @@ struct MnArgs {
 //   Accumulator q, register v of lane 4b + n holds V[j = 64 jb + 16 (b & 3) + 4 v + q]
 //   [r = 4 rb + n] summed over the rows with (i - 64 ib) & 3 == b >> 2; the four row classes
 //   are added once, at the end (everything per sample is linear in V).
-template <int ROLE, bool FULL>
-__device__ __forceinline__ void mnl_body(const MnlGeom& g, const MnArgs& a, float* lds, const int wv,
+template <int ROLE, bool FULL, int SPI>
+__device__ __forceinline__ void mnl_body(const MnlGeom& g, const MnArgs& a, const int64_t* __restrict__ lab,
+                                         const float* __restrict__ class_w, float* lds, const int wv,
                                          const int lane) {
   const int t = threadIdx.x;
   const int I = g.I, J = g.J, R = g.R, C = g.C;
   const int SPF = I * J;
-  float* sZ = lds + g.oZ;  // [2][16][4] Z partials of the A-units (unused entries stay zero)
+  float* sZ = lds + g.oZ;  // [2][SPI][16][4] Z partials of the A-units (unused entries stay zero)
   const float* P0 = a.phi;
   const float* P1 = a.phi + g.offP1;
   const float* PC = a.phi + g.offPC;
@@ -205,9 +217,15 @@ __device__ __forceinline__ void mnl_body(const MnlGeom& g, const MnArgs& a, floa
       bop[s] = (rqv && k < klen) ? P0[(int64_t)(64 * ib + k) * R + rq] : 0.f;
     }
   }
+  // pairs: Wv needs 4 ranks per member but a member has 2 rows: two passes of rows (rank
+  // q = 2 pass + (g & 1)), weights pcp0 / pcp1
+  float pcp0 = 0.f, pcp1 = 0.f;
   if (ROLE != MN_ROLE_IDLE) {
     const int r = 4 * rb + grow;
     pcg = (cok && r < R) ? a.w[r] * PC[c * R + r] : 0.f;
+    const int r0 = 4 * rb + (grow & 1), r1 = 4 * rb + 2 + (grow & 1);
+    pcp0 = (cok && r0 < R) ? a.w[r0] * PC[c * R + r0] : 0.f;
+    pcp1 = (cok && r1 < R) ? a.w[r1] * PC[c * R + r1] : 0.f;
   }
 
   // LDS-DMA map: wave wv issues groups gi (64 chunks = 1 KiB each) = wv + 8 gi of every sample
@@ -233,154 +251,249 @@ __device__ __forceinline__ void mnl_body(const MnlGeom& g, const MnArgs& a, floa
     if (goff[gi] >= 0) mn_dma16(a.X + n * a.xld + goff[gi], lds + (int64_t)buf * SPF + (wv + MN_NW * gi) * 256);
   };
 
-  for (int e = t; e < 2 * 16 * 4; e += MN_T) sZ[e] = 0.f;
+  for (int e = t; e < 4 * 16 * 4; e += MN_T) sZ[e] = 0.f;
   __syncthreads();
   // Retire every register load of the prologue with a wait the compiler sees: otherwise values
   // first used inside the loop keep a conservative s_waitcnt vmcnt(0) in the loop body, which
   // would also drain the LDS-DMA ring on every sample.
   __builtin_amdgcn_s_waitcnt(0);
   const int nbuf = g.nbuf;
-  for (int64_t k = 0; k < nbuf - 1 && k < nr; ++k)
-#pragma unroll
-    for (int gi = 0; gi < kMnlGMax; ++gi)
-      if (gi < gcnt) issue_group(sample_of(k), (int)k, gi);
 
-  mn_f32x4 acc[4], gacc[4];  // A: acc[0] = T of the current sample, gacc[0]; B: all four
+  mn_f32x4 gacc[4];  // A: gacc[0] (rows x ranks of dPhi0); B: all four (dPhi1 by row class)
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    acc[q] = mn_f32x4{0.f, 0.f, 0.f, 0.f};
-    gacc[q] = mn_f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-  float us0 = 0.f, us1 = 0.f, us2 = 0.f, us3 = 0.f;  // A: U partial of the current sample (ranks 4 rb + q)
-  float dpc = 0.f;                                 // A: dPhiC[c][4 rb + grow]
+  for (int q = 0; q < 4; ++q) gacc[q] = mn_f32x4{0.f, 0.f, 0.f, 0.f};
+  float dpc = 0.f;  // A: dPhiC[c][4 rb + grow]
   double lsum = 0.0;
-  int64_t y_cur = 0;
-  float cw_cur = 0.f;
   const float NEG = -__builtin_huge_valf();
+  const int l3 = lane & 3;
+
+  // GEMM of the sample in ring slot `buf`: A-units T (summed into acc[0]) and their Z partial
+  // -> sZ[zidx]; B-units V (acc[0..3]).  u0..u3: the A-unit's U partial (ranks 4 rb + q).
+  auto gemm1 = [&](int buf, int zidx, mn_f32x4(&acc)[4], float& u0, float& u1, float& u2, float& u3) {
+    const float* sb = lds + (int64_t)buf * SPF;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] = mn_f32x4{0.f, 0.f, 0.f, 0.f};
+    float4 xr[16];
+    if (ROLE == MN_ROLE_A) {
+      int row = 64 * ib + lane;
+      if (!FULL) row = row < I ? row : I - 1;
+      const float* rp = sb + row * J;
+      const int sw = row & g.smask;
+#pragma unroll
+      for (int c4 = 0; c4 < 16; ++c4)
+        if (FULL || 4 * c4 < klen) xr[c4] = *reinterpret_cast<const float4*>(rp + 4 * ((16 * jb + c4) ^ sw));
+#pragma unroll
+      for (int c4 = 0; c4 < 16; ++c4) {
+        if (FULL || 4 * c4 < klen) {
+          acc[0] = mfma_4x4(xr[c4].x, bop[4 * c4 + 0], acc[0]);
+          acc[1] = mfma_4x4(xr[c4].y, bop[4 * c4 + 1], acc[1]);
+          acc[2] = mfma_4x4(xr[c4].z, bop[4 * c4 + 2], acc[2]);
+          acc[3] = mfma_4x4(xr[c4].w, bop[4 * c4 + 3], acc[3]);
+        }
+      }
+      acc[0] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+      float u = phiU[0] * acc[0].x;
+      u = fmaf(phiU[1], acc[0].y, u);
+      u = fmaf(phiU[2], acc[0].z, u);
+      u = fmaf(phiU[3], acc[0].w, u);
+      u += dpp_f<0x124>(u);  // row_ror:4
+      u += dpp_f<0x128>(u);  // row_ror:8
+      u += __shfl_xor(u, 16, TR_WAVE);
+      u += __shfl_xor(u, 32, TR_WAVE);
+      u0 = rdl(u, 0);
+      u1 = rdl(u, 1);
+      u2 = rdl(u, 2);
+      u3 = rdl(u, 3);
+      float zpart = wpc[0] * u0;
+      zpart = fmaf(wpc[1], u1, zpart);
+      zpart = fmaf(wpc[2], u2, zpart);
+      zpart = fmaf(wpc[3], u3, zpart);
+      if (lane < 16) sZ[(zidx * 16 + lane) * 4 + wv] = zpart;
+    } else {
+      int cq = 16 * jb + c;
+      if (!FULL) cq = cq < g.JQ ? cq : g.JQ - 1;
+#pragma unroll
+      for (int st = 0; st < 16; ++st) {
+        if (FULL || 4 * st < klen) {
+          int i = 64 * ib + 4 * st + grow;
+          if (!FULL) i = i < I ? i : I - 1;
+          xr[st] = *reinterpret_cast<const float4*>(sb + i * J + 4 * (cq ^ (i & g.smask)));
+        }
+      }
+#pragma unroll
+      for (int st = 0; st < 16; ++st) {
+        if (FULL || 4 * st < klen) {
+          acc[0] = mfma_4x4(xr[st].x, bop[st], acc[0]);
+          acc[1] = mfma_4x4(xr[st].y, bop[st], acc[1]);
+          acc[2] = mfma_4x4(xr[st].z, bop[st], acc[2]);
+          acc[3] = mfma_4x4(xr[st].w, bop[st], acc[3]);
+        }
+      }
+    }
+  };
+  // double softmax + weighted CE of the 16-lane row (lane c = class): returns dZ[c], adds wave
+  // 0's loss term for the lanes `loss_lanes` select
+  auto softmax_ce = [&](float z, int64_t y, float cw, bool loss_lanes) -> float {
+    const float zz = cok ? z : NEG;
+    const float mx = row_max16(zz);
+    const float ez = cok ? expf(zz - mx) : 0.f;
+    const float sum = row_sum16(ez);
+    const float S = ez * (1.0f / sum);  // softmax (model, multinomial…py:187)
+    const float m2 = row_max16(cok ? S : NEG);
+    const float q = cok ? expf(S - m2) : 0.f;
+    const float s2 = row_sum16(q);
+    const bool is_y = cok && (int64_t)c == y;
+    const float dS = cok ? (q * (1.0f / s2) - (is_y ? 1.0f : 0.0f)) * (cw * a.scale) : 0.f;
+    const float dot = row_sum16(dS * S);
+    if (ROLE == MN_ROLE_A) {
+      const float ce = -((S - m2) - logf(s2));  // CrossEntropyLoss on the probabilities
+      lsum += (wv == 0 && is_y && loss_lanes) ? (double)cw * (double)ce : 0.0;
+    }
+    return cok ? S * (dS - dot) : 0.f;
+  };
 #if TR_MNL_PROFILE
   unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long prof_t = __builtin_readcyclecounter();
 #endif
 
-  for (int64_t k = 0; k <= nr; ++k) {
-    if (k < nr) {
-      int64_t ahead = nr - 1 - k;
-      if (ahead > nbuf - 2) ahead = nbuf - 2;
-      mn_wait_vm(gcnt * (int)ahead);  // sample k has landed (this wave's pieces)
-    }
-    TR_MNL_MARK(0);
-    mn_barrier();  // every wave's pieces of sample k; Z partials of k - 1; slot (k - 1) % nbuf free
-    TR_MNL_MARK(1);
-    const bool pre = k + nbuf - 1 < nr;  // refill slot (k - 1) % nbuf with sample k + nbuf - 1
-    const int64_t npre = pre ? sample_of(k + nbuf - 1) : 0;
-    const int bpre = (int)((k + nbuf - 1) % nbuf);
-    if (ROLE == MN_ROLE_IDLE || k >= nr) {
-      if (pre)
+  if constexpr (SPI == 1) {
+    // ---- one sample per barrier: epilogue of k-1, then GEMM of k ----
+    for (int64_t k = 0; k < nbuf - 1 && k < nr; ++k)
+#pragma unroll
+      for (int gi = 0; gi < kMnlGMax; ++gi)
+        if (gi < gcnt) issue_group(sample_of(k), (int)k, gi);
+    mn_f32x4 accP[4], accC[4];
+    float uP0 = 0.f, uP1 = 0.f, uP2 = 0.f, uP3 = 0.f, uC0 = 0.f, uC1 = 0.f, uC2 = 0.f, uC3 = 0.f;
+    int64_t yP = 0, yC = 0;
+    float cwP = 0.f, cwC = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) accP[q] = accC[q] = mn_f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int64_t k = 0; k <= nr; ++k) {
+      if (k < nr) {
+        int64_t ahead = nr - 1 - k;
+        if (ahead > nbuf - 2) ahead = nbuf - 2;
+        mn_wait_vm(gcnt * (int)ahead);  // sample k has landed (this wave's pieces)
+      }
+      TR_MNL_MARK(0);
+      mn_barrier();  // every wave's pieces of sample k; Z partials of k - 1; slot (k - 1) % nbuf free
+      TR_MNL_MARK(1);
+      if (k + nbuf - 1 < nr) {
+        const int64_t npre = sample_of(k + nbuf - 1);
+        const int bpre = (int)((k + nbuf - 1) % nbuf);
 #pragma unroll
         for (int gi = 0; gi < kMnlGMax; ++gi)
           if (gi < gcnt) issue_group(npre, bpre, gi);
-    }
-    TR_MNL_MARK(2);
-
-    if (ROLE != MN_ROLE_IDLE && k >= 1) {  // ---- epilogue of sample k - 1 ----
-      const int slot = (int)((k - 1) & 1);
-      const float4 zp = *reinterpret_cast<const float4*>(sZ + (slot * 16 + c) * 4);
-      const float z = ((zp.x + zp.y) + zp.z) + zp.w;
-      // softmax (model, multinomial…py:187) then CrossEntropyLoss(weight) on the probabilities
-      const float zz = cok ? z : NEG;
-      const float mx = row_max16(zz);
-      const float ez = cok ? expf(zz - mx) : 0.f;
-      const float sum = row_sum16(ez);
-      const float S = ez * (1.0f / sum);
-      const float m2 = row_max16(cok ? S : NEG);
-      const float q = cok ? expf(S - m2) : 0.f;
-      const float s2 = row_sum16(q);
-      const bool is_y = cok && (int64_t)c == y_cur;
-      const float dS = cok ? (q * (1.0f / s2) - (is_y ? 1.0f : 0.0f)) * (cw_cur * a.scale) : 0.f;
-      const float dot = row_sum16(dS * S);
-      const float dz = cok ? S * (dS - dot) : 0.f;
-      // Wv[4 rb + g] = sum_c dZ[c] w PhiC[c][4 rb + g] in DPP row g, then per lane rank 4 rb + (l & 3)
-      const float wrow = row_sum16(dz * pcg);
-      const float w0 = rdl(wrow, 0), w1 = rdl(wrow, 16), w2 = rdl(wrow, 32), w3 = rdl(wrow, 48);
-      const int l3 = lane & 3;
-      const float wvl = l3 == 0 ? w0 : l3 == 1 ? w1 : l3 == 2 ? w2 : w3;
-      if (ROLE == MN_ROLE_A) {
-        gacc[0] += wvl * acc[0];
-        const float ug = grow == 0 ? us0 : grow == 1 ? us1 : grow == 2 ? us2 : us3;
-        dpc = fmaf(dz, wg * ug, dpc);
-        if (wv == 0 && is_y && lane < 16) {
-          const float lse = logf(s2);
-          lsum += (double)cw_cur * (double)(-((S - m2) - lse));
-        }
-      } else {
-#pragma unroll
-        for (int qq = 0; qq < 4; ++qq) gacc[qq] += wvl * acc[qq];
       }
-    }
-    TR_MNL_MARK(3);
-
-    if (ROLE != MN_ROLE_IDLE && k < nr) {  // ---- GEMM of sample k (refill DMA interleaved) ----
-      const int64_t n = sample_of(k);
-      y_cur = a.lab[n];
-      cw_cur = a.class_w[y_cur];
-      const float* sb = lds + (int64_t)(k % nbuf) * SPF;
+      TR_MNL_MARK(2);
+      if (ROLE != MN_ROLE_IDLE) {
+        if (k >= 1) {
+          const int zs = (int)((k - 1) & 1);
+          const float4 zp = *reinterpret_cast<const float4*>(sZ + (zs * 16 + c) * 4);
+          const float dz = softmax_ce(((zp.x + zp.y) + zp.z) + zp.w, yP, cwP, lane < 16);
+          // Wv[4 rb + g] = sum_c dZ[c] w PhiC[c][4 rb + g] in DPP row g; lane rank 4 rb + (l & 3)
+          const float wrow = row_sum16(dz * pcg);
+          const float w0 = rdl(wrow, 0), w1 = rdl(wrow, 16), w2 = rdl(wrow, 32), w3 = rdl(wrow, 48);
+          const float wvl = l3 == 0 ? w0 : l3 == 1 ? w1 : l3 == 2 ? w2 : w3;
+          if (ROLE == MN_ROLE_A) {
+            gacc[0] += wvl * accP[0];
+            const float ug = grow == 0 ? uP0 : grow == 1 ? uP1 : grow == 2 ? uP2 : uP3;
+            dpc = fmaf(dz, wg * ug, dpc);
+          } else {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) acc[q] = mn_f32x4{0.f, 0.f, 0.f, 0.f};
-      if (ROLE == MN_ROLE_A) {
-        int row = 64 * ib + lane;
-        if (!FULL) row = row < I ? row : I - 1;
-        const float* rp = sb + row * J;
-        const int sw = row & g.smask;
-#pragma unroll
-        for (int c4 = 0; c4 < 16; ++c4) {
-          if (FULL || 4 * c4 < klen) {
-            const float4 x = *reinterpret_cast<const float4*>(rp + 4 * ((16 * jb + c4) ^ sw));
-            acc[0] = mfma_4x4(x.x, bop[4 * c4 + 0], acc[0]);
-            acc[1] = mfma_4x4(x.y, bop[4 * c4 + 1], acc[1]);
-            acc[2] = mfma_4x4(x.z, bop[4 * c4 + 2], acc[2]);
-            acc[3] = mfma_4x4(x.w, bop[4 * c4 + 3], acc[3]);
+            for (int qq = 0; qq < 4; ++qq) gacc[qq] += wvl * accP[qq];
           }
-          if ((c4 & 1) == 0 && (c4 >> 1) < gcnt && pre) issue_group(npre, bpre, c4 >> 1);
         }
-        acc[0] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-      } else {
-        int cq = 16 * jb + c;
-        if (!FULL) cq = cq < g.JQ ? cq : g.JQ - 1;
+        if (k < nr) {
+          yC = lab[sample_of(k)];
+          cwC = class_w[yC];
+          gemm1((int)(k % nbuf), (int)(k & 1), accC, uC0, uC1, uC2, uC3);
 #pragma unroll
-        for (int st = 0; st < 16; ++st) {
-          if (FULL || 4 * st < klen) {
-            int i = 64 * ib + 4 * st + grow;
-            if (!FULL) i = i < I ? i : I - 1;
-            const float4 x = *reinterpret_cast<const float4*>(sb + i * J + 4 * (cq ^ (i & g.smask)));
-            acc[0] = mfma_4x4(x.x, bop[st], acc[0]);
-            acc[1] = mfma_4x4(x.y, bop[st], acc[1]);
-            acc[2] = mfma_4x4(x.z, bop[st], acc[2]);
-            acc[3] = mfma_4x4(x.w, bop[st], acc[3]);
-          }
-          if ((st & 1) == 0 && (st >> 1) < gcnt && pre) issue_group(npre, bpre, st >> 1);
+          for (int q = 0; q < 4; ++q) accP[q] = accC[q];
+          uP0 = uC0;
+          uP1 = uC1;
+          uP2 = uC2;
+          uP3 = uC3;
+          yP = yC;
+          cwP = cwC;
         }
       }
       TR_MNL_MARK(4);
-      if (ROLE == MN_ROLE_A) {  // U partial (ranks 4 rb + q) -> this unit's Z partial
-        float u = phiU[0] * acc[0].x;
-        u = fmaf(phiU[1], acc[0].y, u);
-        u = fmaf(phiU[2], acc[0].z, u);
-        u = fmaf(phiU[3], acc[0].w, u);
-        u += dpp_f<0x124>(u);  // row_ror:4
-        u += dpp_f<0x128>(u);  // row_ror:8
-        u += __shfl_xor(u, 16, TR_WAVE);
-        u += __shfl_xor(u, 32, TR_WAVE);
-        us0 = rdl(u, 0);
-        us1 = rdl(u, 1);
-        us2 = rdl(u, 2);
-        us3 = rdl(u, 3);
-        float zpart = wpc[0] * us0;
-        zpart = fmaf(wpc[1], us1, zpart);
-        zpart = fmaf(wpc[2], us2, zpart);
-        zpart = fmaf(wpc[3], us3, zpart);
-        if (lane < 16) sZ[((int)(k & 1) * 16 + lane) * 4 + wv] = zpart;
+    }
+  } else {
+    // ---- two samples (a pair) per barrier: ring slots 2 (p % nps) + h, member h in 16-lane
+    // rows 2h, 2h+1 of the epilogue (both members' softmax chains in the same instructions) ----
+    const int nps = nbuf / 2;
+    const int64_t np = (nr + 1) / 2;
+    // an odd range's last pair repeats the last sample with class weight 0 (contributes 0)
+    auto member_sample = [&](int64_t kk) -> int64_t { return sample_of(kk < nr ? kk : nr - 1); };
+    auto issue_pair = [&](int64_t p) {
+      const int s0 = 2 * (int)(p % nps);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int64_t n = member_sample(2 * p + h);
+#pragma unroll
+        for (int gi = 0; gi < kMnlGMax; ++gi)
+          if (gi < gcnt) issue_group(n, s0 + h, gi);
       }
-      TR_MNL_MARK(5);
+    };
+    for (int64_t p = 0; p < nps - 1 && p < np; ++p) issue_pair(p);
+    mn_f32x4 accA[4], accB[4];  // members a, b of the previous pair (GEMM output of this pair)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) accA[q] = accB[q] = mn_f32x4{0.f, 0.f, 0.f, 0.f};
+    float ua0 = 0.f, ua1 = 0.f, ua2 = 0.f, ua3 = 0.f, ub0 = 0.f, ub1 = 0.f, ub2 = 0.f, ub3 = 0.f;
+    int64_t ya = 0, yb = 0;
+    float cwa = 0.f, cwb = 0.f;
+    const int h = lane >> 5;  // epilogue member of this lane
+    for (int64_t p = 0; p <= np; ++p) {
+      if (p < np) {
+        int64_t ahead = np - 1 - p;
+        if (ahead > nps - 2) ahead = nps - 2;
+        mn_wait_vm(2 * gcnt * (int)ahead);  // pair p has landed (this wave's pieces)
+      }
+      TR_MNL_MARK(0);
+      mn_barrier();  // every wave's pieces of pair p; Z partials of p - 1; slots of pair p - 1 free
+      TR_MNL_MARK(1);
+      if (p + nps - 1 < np) issue_pair(p + nps - 1);
+      TR_MNL_MARK(2);
+      if (ROLE != MN_ROLE_IDLE) {
+        if (p >= 1) {
+          const int zs = (int)((p - 1) & 1);
+          const float4 zp = *reinterpret_cast<const float4*>(sZ + ((zs * 2 + h) * 16 + c) * 4);
+          const int64_t yh = h ? yb : ya;
+          const float cwh = h ? cwb : cwa;
+          const float dz = softmax_ce(((zp.x + zp.y) + zp.z) + zp.w, yh, cwh, (lane & 31) < 16);
+          const float s0 = row_sum16(dz * pcp0), s1 = row_sum16(dz * pcp1);
+          // member a: ranks q = 0, 1 in rows 0, 1 of pass 0; q = 2, 3 of pass 1; member b rows 2, 3
+          const float wa = l3 == 0 ? rdl(s0, 0) : l3 == 1 ? rdl(s0, 16) : l3 == 2 ? rdl(s1, 0) : rdl(s1, 16);
+          const float wb = l3 == 0 ? rdl(s0, 32) : l3 == 1 ? rdl(s0, 48) : l3 == 2 ? rdl(s1, 32) : rdl(s1, 48);
+          if (ROLE == MN_ROLE_A) {
+            gacc[0] += wa * accA[0];
+            gacc[0] += wb * accB[0];
+            const float dzo = __shfl_xor(dz, 32, TR_WAVE);  // the other member's dZ[c]
+            const float dza = h ? dzo : dz, dzb = h ? dz : dzo;
+            const float uga = grow == 0 ? ua0 : grow == 1 ? ua1 : grow == 2 ? ua2 : ua3;
+            const float ugb = grow == 0 ? ub0 : grow == 1 ? ub1 : grow == 2 ? ub2 : ub3;
+            dpc = fmaf(dza, wg * uga, dpc);
+            dpc = fmaf(dzb, wg * ugb, dpc);
+          } else {
+#pragma unroll
+            for (int qq = 0; qq < 4; ++qq) {
+              gacc[qq] += wa * accA[qq];
+              gacc[qq] += wb * accB[qq];
+            }
+          }
+        }
+        if (p < np) {
+          const int s0 = 2 * (int)(p % nps), zs = (int)(p & 1);
+          ya = lab[member_sample(2 * p)];
+          cwa = class_w[ya];
+          yb = lab[member_sample(2 * p + 1)];
+          cwb = 2 * p + 1 < nr ? class_w[yb] : 0.f;
+          gemm1(s0, zs * 2, accA, ua0, ua1, ua2, ua3);
+          gemm1(s0 + 1, zs * 2 + 1, accB, ub0, ub1, ub2, ub3);
+        }
+      }
+      TR_MNL_MARK(4);
     }
   }
 #if TR_MNL_PROFILE
@@ -439,25 +552,29 @@ __device__ __forceinline__ void mnl_body(const MnlGeom& g, const MnArgs& a, floa
   for (int64_t e = t; e < g.slab; e += MN_T) slab[e] = sG[e];
 }
 
-template <bool FULL>
-__global__ __launch_bounds__(MN_T) void k_mnl_fused(MnlGeom g, MnArgs a, const int32_t* __restrict__ stop) {
+template <bool FULL, int SPI>
+__global__ __launch_bounds__(MN_T) void k_mnl_fused(MnlGeom g, MnArgs a, const int64_t* __restrict__ lab,
+                                                    const float* __restrict__ class_w,
+                                                    const int32_t* __restrict__ stop) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   if (stop != nullptr && *stop != 0) return;
   const int lane = threadIdx.x & (TR_WAVE - 1);
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / TR_WAVE);  // wave-uniform
   if (wv < g.nA)
-    mnl_body<MN_ROLE_A, FULL>(g, a, lds, wv, lane);
+    mnl_body<MN_ROLE_A, FULL, SPI>(g, a, lab, class_w, lds, wv, lane);
   else if (wv < g.nunits)
-    mnl_body<MN_ROLE_B, FULL>(g, a, lds, wv, lane);
+    mnl_body<MN_ROLE_B, FULL, SPI>(g, a, lab, class_w, lds, wv, lane);
   else
-    mnl_body<MN_ROLE_IDLE, FULL>(g, a, lds, wv, lane);
+    mnl_body<MN_ROLE_IDLE, FULL, SPI>(g, a, lab, class_w, lds, wv, lane);
 }
 
 // ------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------
 static const void* mnl_kernel(const MnlGeom& g) {
-  return g.full ? reinterpret_cast<const void*>(&k_mnl_fused<true>) : reinterpret_cast<const void*>(&k_mnl_fused<false>);
+  if (g.spi == 2)
+    return g.full ? reinterpret_cast<const void*>(&k_mnl_fused<true, 2>) : reinterpret_cast<const void*>(&k_mnl_fused<false, 2>);
+  return g.full ? reinterpret_cast<const void*>(&k_mnl_fused<true, 1>) : reinterpret_cast<const void*>(&k_mnl_fused<false, 1>);
 }
 
 bool mnl_geom_init(MnlGeom* g, int64_t I, int64_t J, int R, int C, std::string* why) {
@@ -497,12 +614,16 @@ bool mnl_geom_init(MnlGeom* g, int64_t I, int64_t J, int R, int C, std::string* 
   int nbuf = (int)((128 * 1024) / sb);
   if (nbuf > 8) nbuf = 8;
   if (nbuf < 2) nbuf = 2;
-  const int64_t small = 2LL * 16 * 4 + 64;
+  const int64_t small = 4LL * 16 * 4 + 64;
   while (nbuf > 2 && nbuf * I * J + small > 160 * 1024 / 4) --nbuf;
+  // two samples per barrier when the ring holds at least two pairs (TR_MNL_SPI=1 forces one)
+  const char* spi_env = std::getenv("TR_MNL_SPI");
+  g->spi = (nbuf >= 4 && !(spi_env != nullptr && std::atoi(spi_env) == 1)) ? 2 : 1;
+  if (g->spi == 2) nbuf &= ~1;
   g->nbuf = nbuf;
   int64_t o = (int64_t)nbuf * I * J;
   g->oZ = (int)o;
-  o += 2LL * 16 * 4;
+  o += 4LL * 16 * 4;
   if (g->slab <= (int64_t)nbuf * I * J) {
     g->oG = 0;  // the arena image aliases the (drained) ring at the end
   } else {
@@ -538,10 +659,19 @@ hipError_t launch_mnl_fused(const MnlGeom& g, int grid, const float* X, int64_t 
   if (grid < 1 || rows_per_wg < 0 || xld % 4 != 0 || (int64_t)grid * rows_per_wg < N) return hipErrorInvalidValue;
   const size_t lds = (size_t)g.lds_floats * 4;
 MnArgs a{X, N, xld, phi, w, lab, class_w, scale, gpart, dpart, rows_per_wg, reverse};
-  if (g.full)
-    hipLaunchKernelGGL((k_mnl_fused<true>), dim3(grid), dim3(MN_T), lds, st, g, a, stop);
-  else
-    hipLaunchKernelGGL((k_mnl_fused<false>), dim3(grid), dim3(MN_T), lds, st, g, a, stop);
+#define TR_MNL_LAUNCH(F, S) hipLaunchKernelGGL((k_mnl_fused<F, S>), dim3(grid), dim3(MN_T), lds, st, g, a, lab, class_w, stop)
+  if (g.spi == 2) {
+    if (g.full)
+      TR_MNL_LAUNCH(true, 2);
+    else
+      TR_MNL_LAUNCH(false, 2);
+  } else {
+    if (g.full)
+      TR_MNL_LAUNCH(true, 1);
+    else
+      TR_MNL_LAUNCH(false, 1);
+  }
+#undef TR_MNL_LAUNCH
   return hipGetLastError();
 }
 

@@ -32,10 +32,11 @@ RTOL = 1e-5
 @contextlib.contextmanager
 def path(kind):
     """kind: 'auto' (plan's choice: single pass / MFMA forward where eligible), 'twopass'
-    (force the two-pass kernels: linear rows/cols, multinomial MFMA forward + cols) or 'valu'
-    (multinomial: two-pass with the VALU forward)."""
+    (force the two-pass kernels: linear rows/cols, multinomial MFMA forward + cols), 'valu'
+    (multinomial: two-pass with the VALU forward) or 'spi1' (multinomial single pass with one
+    sample per barrier instead of pairs)."""
     from tensor_regression_amd import standard_tensor_regression as S
-    saved = {k: os.environ.get(k) for k in ("TR_FORCE_TWOPASS", "TR_NO_MFMA")}
+    saved = {k: os.environ.get(k) for k in ("TR_FORCE_TWOPASS", "TR_NO_MFMA", "TR_MNL_SPI")}
     for k in saved:
         os.environ.pop(k, None)
     if kind == "twopass":
@@ -43,6 +44,8 @@ def path(kind):
     if kind == "valu":
         os.environ["TR_FORCE_TWOPASS"] = "1"
         os.environ["TR_NO_MFMA"] = "1"
+    if kind == "spi1":
+        os.environ["TR_MNL_SPI"] = "1"
     S._plan_cache.clear()
     try:
         yield
@@ -139,7 +142,7 @@ def test_linear_golden(name, kind):
             _assert_factors(model.Bcp, d["Bcp_final2_list"])
 
 
-@pytest.mark.parametrize("kind", ["auto", "twopass", "valu"])
+@pytest.mark.parametrize("kind", ["auto", "spi1", "twopass", "valu"])
 @pytest.mark.parametrize("name", MNL)
 def test_multinomial_golden(name, kind):
     with path(kind):
@@ -272,7 +275,7 @@ MNL_SHAPES = [((50, 8, 4), 2, 2), ((200, 16, 8), 10, 4), ((97, 5, 7), 16, 3), ((
               ((90, 8, 8), 1, 2)]
 
 
-@pytest.mark.parametrize("kind", ["auto", "twopass", "valu"])
+@pytest.mark.parametrize("kind", ["auto", "spi1", "twopass", "valu"])
 @pytest.mark.parametrize("shape,C,rank", MNL_SHAPES)
 def test_multinomial_sweep_vs_oracle(shape, C, rank, kind):
     with path(kind):
