@@ -35,14 +35,8 @@
 #include "tr_mnl.h"
 
 
-#ifndef TR_MNL_PRELOAD
-#define TR_MNL_PRELOAD 1  // read a sample's 16 X pieces of a unit into registers before its MFMAs
-#endif
 #ifndef TR_MNL_DMA_IN_GEMM
-#define TR_MNL_DMA_IN_GEMM 0  // issue the ring refill between GEMM steps instead of after the barrier
-#endif
-#ifndef TR_MNL_SPLIT
-#define TR_MNL_SPLIT 1  // B-waves run GEMM before the epilogue (SIMD partners pair matrix / vector work)
+#define TR_MNL_DMA_IN_GEMM 1  // issue the ring refill between GEMM steps instead of after the barrier
 #endif
 #ifndef TR_MNL_PROFILE
 #define TR_MNL_PROFILE 0  // profiling build only: per-phase cycle counts of every wave of WG 0..255
@@ -269,7 +263,11 @@ __device__ __forceinline__ void mnl_body(const MnlGeom& g, const MnArgs& a, cons
 
   // GEMM of the sample in ring slot `buf`: A-units T (summed into acc[0]) and their Z partial
   // -> sZ[zidx]; B-units V (acc[0..3]).  u0..u3: the A-unit's U partial (ranks 4 rb + q).
-  auto gemm1 = [&](int buf, int zidx, mn_f32x4(&acc)[4], float& u0, float& u1, float& u2, float& u3) {
+  // dma_on: also issue this wave's LDS-DMA pieces of sample dma_n into ring slot dma_buf, one
+  // piece every other k step between the MFMAs (a burst of them right after the barrier stalls
+  // on the vector-memory issue queue)
+  auto gemm1 = [&](int buf, int zidx, mn_f32x4(&acc)[4], float& u0, float& u1, float& u2, float& u3, bool dma_on,
+                   int64_t dma_n, int dma_buf) {
     const float* sb = lds + (int64_t)buf * SPF;
 #pragma unroll
     for (int q = 0; q < 4; ++q) acc[q] = mn_f32x4{0.f, 0.f, 0.f, 0.f};
@@ -284,6 +282,7 @@ __device__ __forceinline__ void mnl_body(const MnlGeom& g, const MnArgs& a, cons
         if (FULL || 4 * c4 < klen) xr[c4] = *reinterpret_cast<const float4*>(rp + 4 * ((16 * jb + c4) ^ sw));
 #pragma unroll
       for (int c4 = 0; c4 < 16; ++c4) {
+        if (TR_MNL_DMA_IN_GEMM && dma_on && (c4 & 1) == 0 && (c4 >> 1) < gcnt) issue_group(dma_n, dma_buf, c4 >> 1);
         if (FULL || 4 * c4 < klen) {
           acc[0] = mfma_4x4(xr[c4].x, bop[4 * c4 + 0], acc[0]);
           acc[1] = mfma_4x4(xr[c4].y, bop[4 * c4 + 1], acc[1]);
@@ -322,6 +321,7 @@ __device__ __forceinline__ void mnl_body(const MnlGeom& g, const MnArgs& a, cons
       }
 #pragma unroll
       for (int st = 0; st < 16; ++st) {
+        if (TR_MNL_DMA_IN_GEMM && dma_on && (st & 1) == 0 && (st >> 1) < gcnt) issue_group(dma_n, dma_buf, st >> 1);
         if (FULL || 4 * st < klen) {
           acc[0] = mfma_4x4(xr[st].x, bop[st], acc[0]);
           acc[1] = mfma_4x4(xr[st].y, bop[st], acc[1]);
@@ -377,9 +377,11 @@ __device__ __forceinline__ void mnl_body(const MnlGeom& g, const MnArgs& a, cons
       TR_MNL_MARK(0);
       mn_barrier();  // every wave's pieces of sample k; Z partials of k - 1; slot (k - 1) % nbuf free
       TR_MNL_MARK(1);
-      if (k + nbuf - 1 < nr) {
-        const int64_t npre = sample_of(k + nbuf - 1);
-        const int bpre = (int)((k + nbuf - 1) % nbuf);
+      const bool pre = k + nbuf - 1 < nr;  // refill slot (k - 1) % nbuf with sample k + nbuf - 1
+      const int64_t npre = pre ? sample_of(k + nbuf - 1) : 0;
+      const int bpre = (int)((k + nbuf - 1) % nbuf);
+      const bool pre_in_gemm = TR_MNL_DMA_IN_GEMM && ROLE != MN_ROLE_IDLE && k < nr;
+      if (pre && !pre_in_gemm) {
 #pragma unroll
         for (int gi = 0; gi < kMnlGMax; ++gi)
           if (gi < gcnt) issue_group(npre, bpre, gi);
@@ -406,7 +408,7 @@ __device__ __forceinline__ void mnl_body(const MnlGeom& g, const MnArgs& a, cons
         if (k < nr) {
           yC = lab[sample_of(k)];
           cwC = class_w[yC];
-          gemm1((int)(k % nbuf), (int)(k & 1), accC, uC0, uC1, uC2, uC3);
+          gemm1((int)(k % nbuf), (int)(k & 1), accC, uC0, uC1, uC2, uC3, pre, npre, bpre);
 #pragma unroll
           for (int q = 0; q < 4; ++q) accP[q] = accC[q];
           uP0 = uC0;
@@ -453,7 +455,11 @@ __device__ __forceinline__ void mnl_body(const MnlGeom& g, const MnArgs& a, cons
       TR_MNL_MARK(0);
       mn_barrier();  // every wave's pieces of pair p; Z partials of p - 1; slots of pair p - 1 free
       TR_MNL_MARK(1);
-      if (p + nps - 1 < np) issue_pair(p + nps - 1);
+      const bool pre = p + nps - 1 < np;  // refill the slots of pair p - 1 with pair p + nps - 1
+      const bool pre_in_gemm = TR_MNL_DMA_IN_GEMM && ROLE != MN_ROLE_IDLE && p < np;
+      if (pre && !pre_in_gemm) issue_pair(p + nps - 1);
+      const int64_t pq = p + nps - 1;
+      const int spre = 2 * (int)(pq % nps);
       TR_MNL_MARK(2);
       if (ROLE != MN_ROLE_IDLE) {
         if (p >= 1) {
@@ -483,14 +489,17 @@ __device__ __forceinline__ void mnl_body(const MnlGeom& g, const MnArgs& a, cons
             }
           }
         }
+        TR_MNL_MARK(3);
         if (p < np) {
           const int s0 = 2 * (int)(p % nps), zs = (int)(p & 1);
           ya = lab[member_sample(2 * p)];
           cwa = class_w[ya];
           yb = lab[member_sample(2 * p + 1)];
           cwb = 2 * p + 1 < nr ? class_w[yb] : 0.f;
-          gemm1(s0, zs * 2, accA, ua0, ua1, ua2, ua3);
-          gemm1(s0 + 1, zs * 2 + 1, accB, ub0, ub1, ub2, ub3);
+          gemm1(s0, zs * 2, accA, ua0, ua1, ua2, ua3, pre, pre ? member_sample(2 * pq) : 0, spre);
+          TR_MNL_MARK(5);
+          gemm1(s0 + 1, zs * 2 + 1, accB, ub0, ub1, ub2, ub3, pre, pre ? member_sample(2 * pq + 1) : 0, spre + 1);
+          TR_MNL_MARK(6);
         }
       }
       TR_MNL_MARK(4);

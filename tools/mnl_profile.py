@@ -5,7 +5,8 @@
     TR_HIP_LIB=$PWD/tensor_regression_amd/libtr_hip_mnlprof.so python tools/mnl_profile.py
 
 Phases per wave (__builtin_readcyclecounter deltas, averaged over workgroups, per sample):
-DMA wait, barrier, DMA issue, epilogue, GEMM, U partial.
+DMA wait, barrier, DMA issue, epilogue, rest, GEMM of pair member a, of member b (per-sample
+averages; a pair's phases count once per two samples).
 """
 import ctypes
 import os
@@ -36,8 +37,8 @@ buf = (ctypes.c_ulonglong * (256 * 8 * 8))()
 assert fn(buf) == 0
 a = np.array(buf[:], dtype=np.float64).reshape(256, 8, 8)
 per_wg = (N + 255) // 256
-names = ["DMA wait", "barrier", "DMA issue", "epilogue", "GEMM", "U partial"]
+names = ["DMA wait", "barrier", "DMA issue", "epilogue", "rest", "GEMM a", "GEMM b"]
 print("cycles/sample  " + " ".join(f"{n:>10s}" for n in names) + "      total")
 for w in range(8):
-    v = a[:, w, :6].mean(axis=0) / per_wg
+    v = a[:, w, :7].mean(axis=0) / per_wg
     print(f"wave {w}        " + " ".join(f"{x:10.0f}" for x in v) + f" {v.sum():10.0f}")
