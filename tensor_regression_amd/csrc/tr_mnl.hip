@@ -35,6 +35,9 @@
 #include "tr_mnl.h"
 
 
+#ifndef TR_MNL_DMA_MEMCLOB
+#define TR_MNL_DMA_MEMCLOB 1  // "memory" clobber on the LDS-DMA asm (0: the compiler may move LDS reads across it)
+#endif
 #ifndef TR_MNL_DMA_IN_GEMM
 #define TR_MNL_DMA_IN_GEMM 1  // issue the ring refill between GEMM steps instead of after the barrier
 #endif
@@ -109,7 +112,10 @@ __device__ __forceinline__ void mn_dma16(const float* gsrc, const float* lds_dst
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
                : "=&s"(keep)
                : "v"(gsrc), "s"(a)
-               : "memory");
+#if TR_MNL_DMA_MEMCLOB
+               : "memory"
+#endif
+  );
 }
 // s_waitcnt vmcnt(n) for a wave-uniform runtime n (stricter than asked above 31: still safe)
 __device__ __forceinline__ void mn_wait_vm(int n) {
