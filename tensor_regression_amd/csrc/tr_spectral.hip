@@ -26,9 +26,6 @@
 #ifndef TR_SPEC_SKIP
 #define TR_SPEC_SKIP 0  // profiling ablation only: 1 fwd GEMM, 2 epilogue, 4 grad GEMM, 8 X staging
 #endif
-#ifndef TR_SPEC_AUX
-#define TR_SPEC_AUX 2  // non-temporal X loads (X >> Infinity Cache, read once per iteration)
-#endif
 
 #ifndef TR_SPEC_PROFILE
 #define TR_SPEC_PROFILE 0  // profiling build only: per-phase cycle counts of workgroup 0..255
@@ -115,6 +112,30 @@ __device__ __forceinline__ void spec_barrier() {
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 }
+// LDS-DMA pieces (16 B or 4 B per lane to LDS byte address m0 + size * lane) issued from inline
+// asm, so the compiler does not see an LDS write in flight: with the builtin it cannot tell the
+// row block being filled from the one being read and puts an `s_waitcnt vmcnt(0)` in front of the
+// GEMMs' LDS reads, draining the DMA this kernel overlaps with them.  The kernel orders the
+// pieces itself (counted spec_wait_vm + spec_barrier).  m0 is compiler-reserved: saved and
+// restored inside the statement.
+__device__ __forceinline__ uint32_t spec_lds_addr(const float* p) {
+  return (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) float*)p);
+}
+__device__ __forceinline__ void spec_dma16(const float* gsrc, const float* lds_dst) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(spec_lds_addr(lds_dst)))  // wave-uniform
+               : "memory");
+}
+__device__ __forceinline__ void spec_dma4(const float* gsrc, const float* lds_dst) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off nt\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(spec_lds_addr(lds_dst)))  // wave-uniform
+               : "memory");
+}
+
 // s_waitcnt vmcnt(n) for a wave-uniform runtime n (the counter is an immediate)
 __device__ __forceinline__ void spec_wait_vm(int n) {
 #define TR_VM_CASE(k) \
@@ -259,18 +280,13 @@ __global__ __launch_bounds__(kSpecT) void k_spec_fused(
       const int64_t a = r0 >> 2, b = r1 >> 2;  // float4 range (RB*D and W*D are multiples of 4)
       for (int64_t base = a + (int64_t)wv * TR_WAVE; base < b; base += kSpecT) {
         const int64_t e4 = base + lane;
-        if (e4 < b)
-          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + 4 * e4),
-                                           (__attribute__((address_space(3))) void*)(sX + 4 * base), 16, 0,
-                                           TR_SPEC_AUX);
+        if (e4 < b) spec_dma16(src + 4 * e4, sX + 4 * base);
         ++cnt;
       }
     } else {
       for (int64_t base = r0 + (int64_t)wv * TR_WAVE; base < r1; base += kSpecT) {
         const int64_t e = base + lane;
-        if (e < r1)
-          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + e),
-                                           (__attribute__((address_space(3))) void*)(sX + base), 4, 0, TR_SPEC_AUX);
+        if (e < r1) spec_dma4(src + e, sX + base);
         ++cnt;
       }
     }
@@ -306,6 +322,9 @@ __global__ __launch_bounds__(kSpecT) void k_spec_fused(
 
   // y of the next sample is prefetched into a register one iteration ahead (thread o = t < NO)
   float ycur = (MODE == SPEC_TRAIN && nr > 0 && t < NO) ? y[sample_of(0) * NO + t] : 0.f;
+  // retire the prologue's register loads with a wait the compiler sees (values first used in
+  // the loop would otherwise keep a conservative vmcnt(0) inside it)
+  __builtin_amdgcn_s_waitcnt(0);
   if (nr > 0 && !(TR_SPEC_SKIP & 8)) issue_all(sample_of(0));
 
 #if TR_SPEC_PROFILE
