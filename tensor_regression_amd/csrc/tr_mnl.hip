@@ -89,6 +89,24 @@ __device__ __forceinline__ float row_max16(float v) {
   v = fmaxf(v, dpp_f<0x140>(v));
   return v;
 }
+// v_permlane16_swap / v_permlane32_swap (CDNA4) of a value with itself: the two results hold, in
+// every lane, the lane's own row pair / half and the partner's, so their sum is the xor-16 /
+// xor-32 butterfly step without an LDS round trip (ds_bpermute).  Same operand order in every
+// lane: bitwise-identical results across the pair.
+__device__ __forceinline__ float xor16_sum(float v) {
+  const auto q = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(q[0]) + __uint_as_float(q[1]);
+}
+__device__ __forceinline__ float xor32_sum(float v) {
+  const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(q[0]) + __uint_as_float(q[1]);
+}
+// (lower-half value, upper-half value) of v at lane (l mod 32) and (l mod 32) + 32, in every lane
+__device__ __forceinline__ void halves(float v, float& lo, float& hi) {
+  const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  lo = __uint_as_float(q[0]);
+  hi = __uint_as_float(q[1]);
+}
 __device__ __forceinline__ float rfl(float v) {
   return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
 }
@@ -303,8 +321,8 @@ __device__ __forceinline__ void mnl_body(const MnlGeom& g, const MnArgs& a, cons
       u = fmaf(phiU[3], acc[0].w, u);
       u += dpp_f<0x124>(u);  // row_ror:4
       u += dpp_f<0x128>(u);  // row_ror:8
-      u += __shfl_xor(u, 16, TR_WAVE);
-      u += __shfl_xor(u, 32, TR_WAVE);
+      u = xor16_sum(u);
+      u = xor32_sum(u);
       u0 = rdl(u, 0);
       u1 = rdl(u, 1);
       u2 = rdl(u, 2);
@@ -344,12 +362,12 @@ __device__ __forceinline__ void mnl_body(const MnlGeom& g, const MnArgs& a, cons
     const float mx = row_max16(zz);
     const float ez = cok ? expf(zz - mx) : 0.f;
     const float sum = row_sum16(ez);
-    const float S = ez * (1.0f / sum);  // softmax (model, multinomial…py:187)
+    const float S = ez * __builtin_amdgcn_rcpf(sum);  // softmax (model, multinomial…py:187)
     const float m2 = row_max16(cok ? S : NEG);
     const float q = cok ? expf(S - m2) : 0.f;
     const float s2 = row_sum16(q);
     const bool is_y = cok && (int64_t)c == y;
-    const float dS = cok ? (q * (1.0f / s2) - (is_y ? 1.0f : 0.0f)) * (cw * a.scale) : 0.f;
+    const float dS = cok ? (q * __builtin_amdgcn_rcpf(s2) - (is_y ? 1.0f : 0.0f)) * (cw * a.scale) : 0.f;
     const float dot = row_sum16(dS * S);
     if (ROLE == MN_ROLE_A) {
       const float ce = -((S - m2) - logf(s2));  // CrossEntropyLoss on the probabilities
@@ -481,8 +499,8 @@ __device__ __forceinline__ void mnl_body(const MnlGeom& g, const MnArgs& a, cons
           if (ROLE == MN_ROLE_A) {
             gacc[0] += wa * accA[0];
             gacc[0] += wb * accB[0];
-            const float dzo = __shfl_xor(dz, 32, TR_WAVE);  // the other member's dZ[c]
-            const float dza = h ? dzo : dz, dzb = h ? dz : dzo;
+            float dza, dzb;  // both members' dZ[c] in every lane
+            halves(dz, dza, dzb);
             const float uga = grow == 0 ? ua0 : grow == 1 ? ua1 : grow == 2 ? ua2 : ua3;
             const float ugb = grow == 0 ? ub0 : grow == 1 ? ub1 : grow == 2 ? ub2 : ub3;
             dpc = fmaf(dza, wg * uga, dpc);
