@@ -38,6 +38,9 @@
 #ifndef TR_MNL_DMA_MEMCLOB
 #define TR_MNL_DMA_MEMCLOB 1  // "memory" clobber on the LDS-DMA asm (0: the compiler may move LDS reads across it)
 #endif
+#ifndef TR_MNL_SETPRIO
+#define TR_MNL_SETPRIO 0  // s_setprio 1 for waves 4-7 (MI355X_MICROARCH.md, two waves per SIMD item 4)
+#endif
 #ifndef TR_MNL_DMA_IN_GEMM
 #define TR_MNL_DMA_IN_GEMM 1  // issue the ring refill between GEMM steps instead of after the barrier
 #endif
@@ -593,6 +596,9 @@ __global__ __launch_bounds__(MN_T) void k_mnl_fused(MnlGeom g, MnArgs a, const i
   if (stop != nullptr && *stop != 0) return;
   const int lane = threadIdx.x & (TR_WAVE - 1);
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / TR_WAVE);  // wave-uniform
+#if TR_MNL_SETPRIO
+  if (wv >= MN_NW / 2) __builtin_amdgcn_s_setprio(1);  // the younger half loses VALU arbitration
+#endif
   if (wv < g.nA)
     mnl_body<MN_ROLE_A, FULL, SPI>(g, a, lab, class_w, lds, wv, lane);
   else if (wv < g.nunits)
