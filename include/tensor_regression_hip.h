@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define TR_ABI_VERSION 4
+#define TR_ABI_VERSION 5
 
 #define TR_MODEL_LINEAR 0      /* CP_linear_regression: y_hat = <X, [[w; Phi]]> + bias, MSE */
 #define TR_MODEL_MULTINOMIAL 1 /* CP_logistic_regression: softmax(<X, [[w; Phi]]>), CE(weight) */
@@ -170,6 +170,16 @@ int tr_adam_step(tr_plan* plan, float* params, const float* grad, float* exp_avg
                  double beta1, double beta2, double eps, double weight_decay, int amsgrad,
                  int64_t step, double* loss_hist, int64_t hist_base, int64_t iter,
                  int64_t patience, double tol, int32_t* stop_flag, void* stream);
+
+/*
+ * Fold the NEXT iteration's factor preparation into tr_adam_step: with enable = 1, on a plan
+ * that takes the factored multinomial single pass, every tr_adam_step also computes
+ * softplus(A_k) and its derivative from the parameters it has just written, and the following
+ * tr_loss_grad on the SAME params pointer skips its own preparation launch.  Valid as long as
+ * the parameters change only through tr_adam_step between those calls (the fit_Adam loop);
+ * results are bitwise identical to enable = 0.  Other plans ignore the setting.
+ */
+int tr_plan_set_prepare_next(tr_plan* plan, int enable);
 
 /*
  * Spectral model plan (spectral_tensor_regression.CP_linear_regression, spectral…py:424-539;

@@ -9,6 +9,7 @@ the host enqueues `sync_every` iterations between synchronisations.
 """
 import ctypes
 import math
+import os
 
 import numpy as np
 import torch
@@ -17,6 +18,8 @@ from . import _lib
 from ._lib import check, ptr
 
 _DEFAULT_SOFTPLUS = {"beta": 50, "threshold": 1}
+# fit_Adam: fold the next iteration's factor preparation into each Adam step (tests toggle it)
+_PREPARE_NEXT = os.environ.get("TR_NO_PREPARE_NEXT", "0") in ("", "0")
 # torch.optim.Adam defaults (torch/optim/adam.py)
 _ADAM_DEFAULTS = dict(lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0, amsgrad=False,
                       foreach=None, maximize=False, capturable=False, differentiable=False,
@@ -159,6 +162,10 @@ class Plan:
                 for f, shp in enumerate(self.factor_shapes())]
 
     # ---- timing ------------------------------------------------------------------------------
+    def set_prepare_next(self, enable):
+        """tr_plan_set_prepare_next: each adam_step also prepares the next loss_grad's factors."""
+        check(self.lib.tr_plan_set_prepare_next(self.h, 1 if enable else 0), "tr_plan_set_prepare_next")
+
     def set_timing(self, enable, kinds=None):
         """Enable hipEvent timing for the given kernel kinds (names of _lib.KERNEL_KINDS; None = all)."""
         mask = 0
@@ -374,10 +381,31 @@ def run_adam_fit(plan, X, target, class_weight, norm, arena, weights, lambda_L2,
         hist[:base] = torch.tensor(loss_running, dtype=torch.float64)
     stop = torch.zeros(1, dtype=torch.int32, device=dev)
     tmp = torch.zeros_like(grad)
-    ii = 0
-    stopped_at = 0
     if verbose_cb is not None:
         sync_every = 1
+    # the loop changes the arena only through adam_step: let each step prepare the next
+    # iteration's factors (one launch fewer per iteration, bitwise identical results)
+    prep_next = _PREPARE_NEXT and isinstance(plan, Plan) and not isinstance(plan, SpectralPlan)
+    if prep_next:
+        plan.set_prepare_next(True)
+    try:
+        ii, stopped_at = _adam_loop(plan, X, target, class_weight, norm, arena, weights, lambda_L2, max_iter, tol,
+                                    patience, hp, verbose_cb, allreduce, sync_every, grad, m, v, vmax, hist, base,
+                                    stop, tmp)
+    finally:
+        if prep_next:
+            plan.set_prepare_next(False)
+    # stop flag: > 0 plateau convergence after that many iterations; < 0 NaN stop (spectral)
+    n_run = abs(stopped_at) if stopped_at else ii
+    loss_running.extend(hist[base:base + n_run].tolist())
+    plan.last_stop = stopped_at
+    return stopped_at > 0, n_run
+
+
+def _adam_loop(plan, X, target, class_weight, norm, arena, weights, lambda_L2, max_iter, tol, patience, hp,
+               verbose_cb, allreduce, sync_every, grad, m, v, vmax, hist, base, stop, tmp):
+    ii = 0
+    stopped_at = 0
     while ii < max_iter:
         n = min(sync_every, max_iter - ii)
         for k in range(n):
@@ -395,8 +423,4 @@ def run_adam_fit(plan, X, target, class_weight, norm, arena, weights, lambda_L2,
             verbose_cb.after_step(ii - 1, float(hist[base + ii - 1].item()))
         if stopped_at:
             break
-    # stop flag: > 0 plateau convergence after that many iterations; < 0 NaN stop (spectral)
-    n_run = abs(stopped_at) if stopped_at else ii
-    loss_running.extend(hist[base:base + n_run].tolist())
-    plan.last_stop = stopped_at
-    return stopped_at > 0, n_run
+    return ii, stopped_at

@@ -12,7 +12,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TR_HIP_LIB", os.path.join(_HERE, "libtr_hip.so"))
 
-TR_ABI_VERSION = 4
+TR_ABI_VERSION = 5
 TR_MODEL_LINEAR = 0
 TR_MODEL_MULTINOMIAL = 1
 TR_MODEL_SPECTRAL = 2
@@ -48,6 +48,7 @@ SIGNATURES = {
     "tr_adam_step": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _c.c_float, _c.c_double, _c.c_double,
                                 _c.c_double, _c.c_double, _c.c_double, _c.c_int, _c.c_int64, _vp,
                                 _c.c_int64, _c.c_int64, _c.c_int64, _c.c_double, _vp, _vp]),
+    "tr_plan_set_prepare_next": (_c.c_int, [_vp, _c.c_int]),
 }
 
 _lock = threading.Lock()

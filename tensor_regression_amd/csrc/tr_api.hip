@@ -53,6 +53,10 @@ struct tr_plan {
   int64_t slab_stride = 0;
   // two-pass strategy
   int64_t max_slabs = 0;
+  // next-iteration factor preparation folded into tr_adam_step (tr_plan_set_prepare_next)
+  int prep_next = 0;
+  int prepared = 0;  // 1: phi / dphi hold the factors of prep_params
+  const float* prep_params = nullptr;
   // workspace
   void* ws = nullptr;
   size_t ws_bytes = 0;
@@ -565,6 +569,7 @@ extern "C" int64_t tr_plan_workspace_bytes(const tr_plan* p) { return p ? (int64
 extern "C" const char* tr_plan_describe(const tr_plan* p) { return p ? p->desc.c_str() : ""; }
 
 static int factor_prep(tr_plan* p, const float* params, const float* w, const int32_t* stop, hipStream_t st) {
+  p->prepared = 0;
   TimedLaunch tl(p, st, TR_KERNEL_PREP);
   TR_HIP(launch_build_dense(p->fs, params, p->sp_beta, p->sp_thr, p->phi, p->dphi, w, p->dense, stop, st));
   return 0;
@@ -617,6 +622,21 @@ extern "C" int tr_forward(tr_plan* p, const float* X, int64_t n_rows, const floa
   return 0;
 }
 
+// True when the previous tr_adam_step already prepared phi / dphi of exactly these params (the
+// factored multinomial pass needs nothing else); the mark is consumed either way.
+static bool consume_prepared(tr_plan* p, const float* params) {
+  const bool ok = p->prepared && p->prep_params == params;
+  p->prepared = 0;
+  return ok;
+}
+
+extern "C" int tr_plan_set_prepare_next(tr_plan* p, int enable) {
+  if (p == nullptr) return fail(TR_E_ARG, "plan is NULL");
+  p->prep_next = enable ? 1 : 0;
+  p->prepared = 0;
+  return 0;
+}
+
 extern "C" int tr_loss_grad(tr_plan* p, const float* X, int64_t n_rows, const void* target,
                             const float* class_weight, double norm, const float* params, const float* weights,
                             float* grad_out, float* yhat_out, const int32_t* stop_flag, void* stream) {
@@ -653,16 +673,14 @@ extern "C" int tr_loss_grad(tr_plan* p, const float* X, int64_t n_rows, const vo
     {
       TimedLaunch tl(p, st, TR_KERNEL_REDUCE);
       TR_HIP(launch_reduce_slabs(4, p->gpart, p->sgrid, p->slab_stride, p->G, p->dpart, p->sgrid, 1.0 / norm,
-                                 grad_out + p->nparams, nullptr, stop_flag, st));
+                                 grad_out + p->nparams, nullptr, stop_flag, st, p->dphi, grad_out, p->nparams));
     }
-    TimedLaunch tl(p, st, TR_KERNEL_MTTKRP);
-    TR_HIP(launch_spec_chain(p->nparams, p->G, p->dphi, grad_out, stop_flag, st));
     return 0;
   }
   if (p->mnl) {
     const int reverse = (int)(p->parity & 1u);
     p->parity++;
-    {
+    if (!consume_prepared(p, params)) {
       TimedLaunch tl(p, st, TR_KERNEL_PREP);
       TR_HIP(launch_prep_factors(p->fs, params, p->sp_beta, p->sp_thr, p->phi, p->dphi, stop_flag, st));
     }
@@ -676,12 +694,11 @@ extern "C" int tr_loss_grad(tr_plan* p, const float* X, int64_t n_rows, const vo
     {
       TimedLaunch tl(p, st, TR_KERNEL_REDUCE);
       TR_HIP(launch_reduce_slabs(4, p->gpart, grid, p->mg.slab, p->G, p->dpart, grid, 1.0 / norm,
-                                 grad_out + p->nparams, nullptr, stop_flag, st));
+                                 grad_out + p->nparams, nullptr, stop_flag, st, p->dphi, grad_out, p->fs.nfelem));
     }
-    TimedLaunch tl(p, st, TR_KERNEL_MTTKRP);
-    TR_HIP(launch_spec_chain(p->fs.nfelem, p->G, p->dphi, grad_out, stop_flag, st));
     return 0;
   }
+  p->prepared = 0;
   int rc = factor_prep(p, params, weights, stop_flag, st);
   if (rc) return rc;
   const int64_t N = n_rows;
@@ -820,9 +837,24 @@ extern "C" int tr_adam_step(tr_plan* p, float* params, const float* grad, float*
   ua.patience = patience;
   ua.tol = tol;
   ua.nan_stop = p->model == TR_MODEL_SPECTRAL;  // spectral fit_Adam's NaN stop (spectral…py:738-741)
+  // fold the next iteration's factor preparation into this launch (tr_plan_set_prepare_next)
+  PrepArgs pa;
+  std::memset(&pa, 0, sizeof(pa));
+  if (p->prep_next && p->mnl && update_prepare_mode_ok(p->fs, 1)) {
+    pa.mode = 1;
+    pa.beta = p->sp_beta;
+    pa.thr = p->sp_thr;
+    pa.phi = p->phi;
+    pa.dphi = p->dphi;
+  }
+  p->prepared = 0;
   TimedLaunch tl(p, (hipStream_t)stream, TR_KERNEL_UPDATE);
   TR_HIP(launch_update(p->fs, p->has_bias, params, grad, ua, exp_avg, exp_avg_sq, max_exp_avg_sq, nullptr, nullptr,
-                       loss_hist, stop_flag, (hipStream_t)stream));
+                       loss_hist, stop_flag, (hipStream_t)stream, &pa));
+  if (pa.mode > 0) {
+    p->prepared = 1;
+    p->prep_params = params;
+  }
   return 0;
 }
 

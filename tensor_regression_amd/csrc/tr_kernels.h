@@ -31,6 +31,15 @@ struct UpdateArgs {
   int nan_stop;        // spectral fit_Adam: stop (not converged) on a NaN loss while iter <= patience
 };
 
+// Next-iteration factor preparation folded into an Adam step (k_update, tr_plan_set_prepare_next):
+// mode 1 = phi / dphi (k_prep_factors' output; what the factored multinomial pass reads).
+struct PrepArgs {
+  int mode;
+  float beta, thr;
+  float* phi;
+  float* dphi;
+};
+
 // Launch helpers (all asynchronous on `st`).  Return hipError_t of the launch.
 // `xld` is X's row stride in floats (P for a dense X; may differ for strided / windowed views,
 // the P floats of each row being contiguous).
@@ -74,11 +83,15 @@ hipError_t launch_cols(int C, int W, int64_t nstripes, int64_t nchunks, const fl
                        const int32_t* stop, hipStream_t st);
 hipError_t launch_reduce_slabs(int W, const float* part, int64_t nslabs, int64_t ncols, float* out,
                                const double* dpart, int64_t nd, double loss_scale, float* loss_slot,
-                               float* bias_slot, const int32_t* stop, hipStream_t st);
+                               float* bias_slot, const int32_t* stop, hipStream_t st,
+                               const float* chain_dphi = nullptr, float* chain_out = nullptr, int64_t nchain = 0);
 hipError_t launch_mttkrp(const FactorSet& fs, const float* phi, const float* dphi, const float* w,
                          const float* G, float* grad, const int32_t* stop, hipStream_t st);
 hipError_t launch_update(const FactorSet& fs, int n_bias, float* params, const float* grad,
                          const UpdateArgs& ua, float* m, float* v, float* vmax, float* grad_total_out,
-                         float* loss_out, double* loss_hist, int32_t* stop, hipStream_t st);
+                         float* loss_out, double* loss_hist, int32_t* stop, hipStream_t st,
+                         const PrepArgs* prep = nullptr);
+// whether k_update can prepare the next iteration in this mode for this factor set
+bool update_prepare_mode_ok(const FactorSet& fs, int mode);
 
 }  // namespace tr

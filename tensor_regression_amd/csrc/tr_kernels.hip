@@ -19,6 +19,8 @@
 #include "tr_common.h"
 #include "tr_kernels.h"
 
+#include <cstring>
+
 namespace tr {
 
 // ------------------------------------------------------------------------------------------
@@ -669,6 +671,8 @@ __global__ __launch_bounds__(1024) void k_reduce_slabs(const float* __restrict__
                                                        const double* __restrict__ dpart, int64_t nd,
                                                        double loss_scale, float* __restrict__ loss_slot,
                                                        float* __restrict__ bias_slot,
+                                                       const float* __restrict__ chain_dphi,
+                                                       float* __restrict__ chain_out, int64_t nchain,
                                                        const int32_t* __restrict__ stop) {
   using V = VecT<W>;
   using VT = typename V::T;
@@ -703,6 +707,14 @@ __global__ __launch_bounds__(1024) void k_reduce_slabs(const float* __restrict__
 #pragma unroll
     for (int w = 1; w < NWV; ++w) s = V::add(s, sred[w][lane]);
     reinterpret_cast<VT*>(out)[colv] = s;
+    if (chain_out != nullptr) {  // softplus chain of arena-layout slabs (k_spec_chain) fused
+      const float* sv = reinterpret_cast<const float*>(&s);
+#pragma unroll
+      for (int c = 0; c < W; ++c) {
+        const int64_t e = colv * W + c;
+        if (e < nchain) chain_out[e] = sv[c] * chain_dphi[e];
+      }
+    }
   }
   if (blockIdx.x == 0 && dpart != nullptr) {
     double s0 = 0.0, s1 = 0.0;
@@ -914,6 +926,22 @@ __device__ double np_pairwise_sum_absdiff(const double* h, int64_t n) {
   return total;
 }
 
+// Next iteration's factor preparation from the just-updated factors (tr_plan_set_prepare_next):
+// softplus and its derivative, k_prep_factors' arithmetic, from the new values in LDS.
+__device__ void update_prepare_next(const FactorSet& fs, const PrepArgs& pa, const float* snew) {
+  __syncthreads();
+  for (int64_t k = threadIdx.x; k < fs.nfelem; k += blockDim.x) {
+    const float a = snew[k];
+    if (fs.nonneg[tr_factor_of(fs, k)]) {
+      pa.phi[k] = tr_softplus(a, pa.beta, pa.thr);
+      pa.dphi[k] = tr_softplus_grad(a, pa.beta, pa.thr);
+    } else {
+      pa.phi[k] = a;
+      pa.dphi[k] = 1.0f;
+    }
+  }
+}
+
 __global__ __launch_bounds__(1024) void k_update(FactorSet fs, int n_bias, float* __restrict__ params,
                                                  const float* __restrict__ grad, UpdateArgs ua,
                                                  float* __restrict__ m, float* __restrict__ v,
@@ -921,8 +949,9 @@ __global__ __launch_bounds__(1024) void k_update(FactorSet fs, int n_bias, float
                                                  float* __restrict__ grad_total_out,
                                                  float* __restrict__ loss_out,
                                                  double* __restrict__ loss_hist,
-                                                 int32_t* __restrict__ stop) {
+                                                 int32_t* __restrict__ stop, PrepArgs pa) {
 #pragma clang fp contract(off)
+  extern __shared__ __attribute__((aligned(16))) float snew[];  // pa.mode > 0: the new factors
   __shared__ float wsum[TR_MAXF * 16];
   __shared__ float norms[TR_MAXF];
   if (stop != nullptr && *stop != 0) return;
@@ -988,6 +1017,7 @@ __global__ __launch_bounds__(1024) void k_update(FactorSet fs, int n_bias, float
     m[e] = mm;
     v[e] = vv;
     params[e] = p;
+    if (pa.mode > 0 && e < nfe) snew[e] = p;
   }
   if (t == 0) {
     float l2 = 0.f;
@@ -1000,6 +1030,7 @@ __global__ __launch_bounds__(1024) void k_update(FactorSet fs, int n_bias, float
     if (ua.mode == 0 && ua.nan_stop && stop != nullptr && ua.iter <= ua.patience && __builtin_isnan(total))
       *stop = -(int32_t)(ua.iter + 1);
   }
+  if (ua.mode == 0 && pa.mode > 0) update_prepare_next(fs, pa, snew);
 }
 
 
@@ -1213,14 +1244,15 @@ hipError_t launch_cols(int C, int W, int64_t nstripes, int64_t nchunks, const fl
 // ---- slab reduction --------------------------------------------------------------------------
 hipError_t launch_reduce_slabs(int W, const float* part, int64_t nslabs, int64_t ncols, float* out,
                                const double* dpart, int64_t nd, double loss_scale, float* loss_slot,
-                               float* bias_slot, const int32_t* stop, hipStream_t st) {
+                               float* bias_slot, const int32_t* stop, hipStream_t st, const float* chain_dphi,
+                               float* chain_out, int64_t nchain) {
   const unsigned grid = cdiv(ncols / W, TR_WAVE);
   if (W == 4)
     hipLaunchKernelGGL(k_reduce_slabs<4>, dim3(grid), dim3(1024), 0, st, part, nslabs, ncols, out, dpart, nd,
-                       loss_scale, loss_slot, bias_slot, stop);
+                       loss_scale, loss_slot, bias_slot, chain_dphi, chain_out, nchain, stop);
   else
     hipLaunchKernelGGL(k_reduce_slabs<1>, dim3(grid), dim3(1024), 0, st, part, nslabs, ncols, out, dpart, nd,
-                       loss_scale, loss_slot, bias_slot, stop);
+                       loss_scale, loss_slot, bias_slot, chain_dphi, chain_out, nchain, stop);
   return hipGetLastError();
 }
 
@@ -1259,11 +1291,23 @@ hipError_t launch_mttkrp(const FactorSet& fs, const float* phi, const float* dph
   return mttkrp_launch_r<64>(fs, phi, dphi, w, G, grad, use_lds, stop, st, grid, lds);
 }
 
+bool update_prepare_mode_ok(const FactorSet& fs, int mode) {
+  // mode 1 only: the new factors are staged in the update workgroup's LDS.  (Building dense B
+  // there too was measured slower than the separate multi-workgroup k_build_dense: one CU took
+  // 17 us for config 2's 32768 x 8 products.)
+  return mode <= 0 || (mode == 1 && fs.nfelem * 4 <= 48 * 1024);
+}
+
 hipError_t launch_update(const FactorSet& fs, int n_bias, float* params, const float* grad,
                          const UpdateArgs& ua, float* m, float* v, float* vmax, float* grad_total_out,
-                         float* loss_out, double* loss_hist, int32_t* stop, hipStream_t st) {
-  hipLaunchKernelGGL(k_update, dim3(1), dim3(1024), 0, st, fs, n_bias, params, grad, ua, m, v, vmax,
-                     grad_total_out, loss_out, loss_hist, stop);
+                         float* loss_out, double* loss_hist, int32_t* stop, hipStream_t st, const PrepArgs* pa) {
+  PrepArgs p0;
+  std::memset(&p0, 0, sizeof(p0));
+  const PrepArgs& pp = pa != nullptr && ua.mode == 0 ? *pa : p0;
+  if (!update_prepare_mode_ok(fs, pp.mode)) return hipErrorInvalidValue;
+  const size_t lds = pp.mode > 0 ? (size_t)fs.nfelem * 4 : 0;
+  hipLaunchKernelGGL(k_update, dim3(1), dim3(1024), lds, st, fs, n_bias, params, grad, ua, m, v, vmax,
+                     grad_total_out, loss_out, loss_hist, stop, pp);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   if (ua.mode == 0 && loss_hist != nullptr && stop != nullptr && ua.iter > ua.patience && ua.tol > 0.0) {

@@ -487,3 +487,55 @@ def test_process_group_single_rank_matches_local():
         res.append(list(mm.loss_running))
     assert res[0] == res[1]
     dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case", ["fused", "fused_4d", "cluster", "mnl", "mnl_twopass", "amsgrad_converge"])
+def test_prepare_next_bitwise_equals_separate_prep(case):
+    """tr_plan_set_prepare_next: each Adam step (k_update) also prepares the next iteration's
+    softplus factors / dense B, and the next tr_loss_grad skips its preparation launch.  A fit
+    that way is bit-identical to one that prepares inside every tr_loss_grad, on every strategy
+    (including those where the update only prepares phi, or nothing)."""
+    from tensor_regression_amd import CP_linear_regression, CP_logistic_regression
+    from tensor_regression_amd import _engine
+    from tensor_regression_amd import standard_tensor_regression as S
+    g = torch.Generator().manual_seed(23)
+    shape = {"fused": (3000, 64, 32), "fused_4d": (900, 8, 8, 16), "cluster": (700, 64, 64, 32),
+             "mnl": (1500, 128, 64), "mnl_twopass": (800, 8, 6, 10), "amsgrad_converge": (2500, 64, 32)}[case]
+    X = torch.randn(*shape, generator=g).to(DEV)
+    if case.startswith("mnl"):
+        y = torch.randint(0, 6, (shape[0],), generator=g)
+        y[:6] = torch.arange(6)
+        y = y.to(DEV)
+    else:
+        y = torch.randn(shape[0], generator=g).to(DEV)
+    outs = []
+    saved = _engine._PREPARE_NEXT
+    try:
+        for prep in (True, False):
+            _engine._PREPARE_NEXT = prep
+            S._plan_cache.clear()
+            torch.manual_seed(8)
+            if case.startswith("mnl"):
+                nn = [True, False, True] + [False] * (len(shape) - 3)
+                m = CP_logistic_regression(X, y, rank=6, non_negative=nn, device=DEV)
+                conv = m.fit_Adam(lambda_L2=0.01, max_iter=12, tol=0, patience=10, weights=np.ones(6),
+                                  Adam_kwargs={"lr": 0.01})
+            else:
+                rank = 16 if case == "cluster" else 5
+                m = CP_linear_regression(X.shape, rank=rank, non_negative=True, device=DEV)
+                kw, tol = {"lr": 0.01}, 0
+                if case == "amsgrad_converge":
+                    kw, tol = {"lr": 0.05, "amsgrad": True, "weight_decay": 1e-3}, 1e9
+                conv = m.fit_Adam(X, y, lambda_L2=0.01, max_iter=14, tol=tol, patience=4, Adam_kwargs=kw)
+            outs.append((conv, list(m.loss_running), [a.detach().cpu().numpy() for a in m.Bcp], m._plan.describe))
+    finally:
+        _engine._PREPARE_NEXT = saved
+        S._plan_cache.clear()
+    if case == "mnl_twopass":
+        assert "2pass" in outs[0][3], outs[0][3]
+    assert outs[0][0] == outs[1][0]
+    assert outs[0][1] == outs[1][1]
+    if case == "amsgrad_converge":
+        assert outs[0][0] and len(outs[0][1]) == 6
+    for a, b in zip(outs[0][2], outs[1][2]):
+        assert np.array_equal(a, b)
