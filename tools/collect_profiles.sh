@@ -8,6 +8,11 @@ for c in "$@"; do
   cp $src/${c}_bench.json profiles/${round}_${c}_bench.json
   cp $src/${c}_bench_under_rocprof.json profiles/${round}_${c}_bench_under_rocprof.json
   cp $src/trace/${c}_kernel_stats.csv profiles/${round}_${c}_kernel_stats.csv
+  if [ -f $src/${c}_mfma.json ]; then
+    cp $src/${c}_mfma.json profiles/${round}_${c}_mfma.json
+    f=$(ls $src/mfma/${c}*counter_collection.csv | tail -1)
+    { head -1 $f; grep 'tr::' $f || true; } > profiles/${round}_${c}_pmc_mfma.csv
+  fi
   for p in fetch write; do
     f=$(ls $src/$p/${c}*counter_collection.csv | tail -1)
     { head -1 $f; grep 'tr::' $f || true; } > profiles/${round}_${c}_pmc_${p}.csv

@@ -33,6 +33,16 @@ for cfg in "$@"; do
   timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $OUT/write -o $cfg -- \
       python $ROOT/bench.py --config $cfg --steps 10 --warmup 2 --no-cpu-baseline \
       > /dev/null 2> $OUT/${cfg}_write.err || exit 1
+  if [ "$cfg" = c3 ] || [ "$cfg" = c5 ]; then
+    echo "[$cfg] pmc MFMA busy" >&2
+    timeout -k 10 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv \
+        -d $OUT/mfma -o $cfg -- python $ROOT/bench.py --config $cfg --steps 10 --warmup 2 --no-cpu-baseline \
+        > /dev/null 2> $OUT/${cfg}_mfma.err || exit 1
+    # algorithmic flops per launch: c3 factored pass 4*P*R per sample; c5 4*W*D*K per sample
+    case $cfg in c3) fl=17179869184; kre="k_mnl_fused" ;; c5) fl=103884521472; kre="k_spec_fused<0" ;; esac
+    python $ROOT/tools/pmc_mfma.py --config $cfg --csv $(ls $OUT/mfma/${cfg}*counter_collection.csv | tail -1) \
+        --kernel "$kre" --flops $fl --out $OUT/${cfg}_mfma.json || exit 1
+  fi
   python $ROOT/tools/pmc_traffic.py --config $cfg --fetch $(ls $OUT/fetch/${cfg}*counter_collection.csv | tail -1) \
       --write $(ls $OUT/write/${cfg}*counter_collection.csv | tail -1) ${alg:+--algorithmic $alg} --dominant $dom \
       --out $OUT/traffic.json > /dev/null || exit 1
