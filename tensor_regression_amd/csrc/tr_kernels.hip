@@ -749,12 +749,12 @@ __global__ __launch_bounds__(1024) void k_reduce_slabs(const float* __restrict__
 // issued before they are consumed (G is L2-resident, so the loop is latency-, not
 // bandwidth-bound); factor columns sit in LDS; fixed-order block reduction over rank columns.
 // ==========================================================================================
-template <int RMAX, int NO>
+template <int RMAX, int NO, bool USE_LDS>
 __global__ __launch_bounds__(256) void k_mttkrp(FactorSet fs, const float* __restrict__ phi,
                                                 const float* __restrict__ dphi,
                                                 const float* __restrict__ w,
                                                 const float* __restrict__ G, float* __restrict__ out,
-                                                int use_lds, const int32_t* __restrict__ stop) {
+                                                const int32_t* __restrict__ stop) {
   constexpr int U = RMAX >= 64 ? 4 : 8;
   constexpr int NOD = NO > 0 ? NO : 1;
   extern __shared__ __attribute__((aligned(16))) float sphi[];
@@ -770,9 +770,19 @@ __global__ __launch_bounds__(256) void k_mttkrp(FactorSet fs, const float* __res
     ++f;
   }
   const int i = b;
+  // The factors are staged in LDS with an odd row stride S (lanes walking consecutive rows hit
+  // distinct banks; stride R = 8 / 16 put 8 / 16 lanes on one bank), and USE_LDS is a template
+  // parameter so that the reads compile to ds_read rather than generic flat loads.
+  const int S = USE_LDS ? (R | 1) : R;
   const float* F = phi;
-  if (use_lds) {
-    for (int k = threadIdx.x; k < (int)fs.nfelem; k += blockDim.x) sphi[k] = phi[k];
+  if constexpr (USE_LDS) {
+    for (int k = threadIdx.x; k < (int)fs.nfelem; k += blockDim.x) {
+      const int g = tr_factor_of(fs, k);
+      int rows_before = 0;
+      for (int h = 0; h < g; ++h) rows_before += (int)fs.dim[h];
+      const int within = k - (int)fs.off[g];
+      sphi[(rows_before + within / R) * S + within % R] = phi[k];
+    }
     F = sphi;
   }
   if (threadIdx.x < RMAX) sw[threadIdx.x] = threadIdx.x < R ? w[threadIdx.x] : 0.f;
@@ -786,7 +796,13 @@ __global__ __launch_bounds__(256) void k_mttkrp(FactorSet fs, const float* __res
       const int g = fs.others[f][k];
       od[k] = (int)fs.dim[g];
       ostr[k] = (int)fs.stride[g];
-      ooff[k] = (int)fs.off[g];
+      if (USE_LDS) {
+        int rows_before = 0;
+        for (int h = 0; h < g; ++h) rows_before += (int)fs.dim[h];
+        ooff[k] = rows_before * S;
+      } else {
+        ooff[k] = (int)fs.off[g];
+      }
     } else {
       od[k] = 1;
       ostr[k] = 0;
@@ -833,7 +849,7 @@ __global__ __launch_bounds__(256) void k_mttkrp(FactorSet fs, const float* __res
 #pragma unroll
       for (int k = 0; k < NOD; ++k) {
         pos += idx[k] * ostr[k];
-        frow[u][k] = ooff[k] + idx[k] * R;
+        frow[u][k] = ooff[k] + idx[k] * S;
       }
       gv[u] = ok ? G[pos] : 0.f;
       advance();
@@ -1262,8 +1278,11 @@ static hipError_t mttkrp_launch_r(const FactorSet& fs, const float* phi, const f
                                   const float* G, float* grad, int use_lds, const int32_t* stop, hipStream_t st,
                                   dim3 grid, size_t lds) {
   const dim3 block(256);
-#define TR_MTT(NO) \
-  hipLaunchKernelGGL((k_mttkrp<RMAX, NO>), grid, block, lds, st, fs, phi, dphi, w, G, grad, use_lds, stop)
+#define TR_MTT(NO)                                                                                      \
+  if (use_lds)                                                                                          \
+    hipLaunchKernelGGL((k_mttkrp<RMAX, NO, true>), grid, block, lds, st, fs, phi, dphi, w, G, grad, stop); \
+  else                                                                                                  \
+    hipLaunchKernelGGL((k_mttkrp<RMAX, NO, false>), grid, block, lds, st, fs, phi, dphi, w, G, grad, stop)
   switch (fs.nf - 1) {
     case 0: TR_MTT(0); break;
     case 1: TR_MTT(1); break;
@@ -1282,8 +1301,9 @@ hipError_t launch_mttkrp(const FactorSet& fs, const float* phi, const float* dph
                          const float* G, float* grad, const int32_t* stop, hipStream_t st) {
   int64_t rows = 0;
   for (int f = 0; f < fs.nf; ++f) rows += fs.dim[f];
-  const int use_lds = fs.nfelem <= kLdsFactorLimit;
-  const size_t lds = use_lds ? (size_t)fs.nfelem * sizeof(float) : 0;
+  const int64_t padded = rows * (fs.rank | 1);  // odd LDS row stride (k_mttkrp)
+  const int use_lds = padded <= kLdsFactorLimit;
+  const size_t lds = use_lds ? (size_t)padded * sizeof(float) : 0;
   const dim3 grid((unsigned)rows);
   if (fs.rank <= 8) return mttkrp_launch_r<8>(fs, phi, dphi, w, G, grad, use_lds, stop, st, grid, lds);
   if (fs.rank <= 16) return mttkrp_launch_r<16>(fs, phi, dphi, w, G, grad, use_lds, stop, st, grid, lds);
