@@ -93,13 +93,41 @@ def make_data(cfg, rank_id, dev):
     return X, y
 
 
-def cpu_baseline(cfg, X, y, model_init, budget_s=15.0):
-    """Oracle (reference op sequence on torch CPU) on the same X: bounded iterations."""
+def host_cpu_info():
+    """Cores this process may run on (affinity), the machine's logical CPUs and the physical
+    cores among the allowed CPUs (distinct (package, core) pairs in /proc/cpuinfo)."""
+    allowed = sorted(os.sched_getaffinity(0))
+    phys = None
+    try:
+        cores, cur = set(), {}
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if ":" in line:
+                    k, v = (s.strip() for s in line.split(":", 1))
+                    cur[k] = v
+                elif cur:
+                    if int(cur.get("processor", -1)) in allowed:
+                        cores.add((cur.get("physical id"), cur.get("core id")))
+                    cur = {}
+        if cur and int(cur.get("processor", -1)) in allowed:
+            cores.add((cur.get("physical id"), cur.get("core id")))
+        phys = len(cores) or None
+    except (OSError, ValueError):
+        pass
+    return {"affinity_cpus": len(allowed), "os_cpu_count": os.cpu_count(), "physical_cores_allowed": phys,
+            "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS")}
+
+
+def cpu_baseline(cfg, X, y, model_init, budget_s=15.0, threads=None):
+    """Oracle (reference op sequence on torch CPU) on the same X: 2 warm-up + >= 5 timed
+    iterations at the full per-GPU size, on every core this process may run on."""
     from oracle import cp_oracle
+    info = host_cpu_info()
+    nthreads = threads or info["affinity_cpus"]
+    torch.set_num_threads(nthreads)
     Xc = X.cpu()
     yc = y.cpu()
     R = cfg["rank"]
-    t_copy = time.perf_counter()
     lam, adam = 0.01, {"lr": 0.01}
 
     def run(iters):
@@ -115,19 +143,20 @@ def cpu_baseline(cfg, X, y, model_init, budget_s=15.0):
                                       iters, 0.0, 10, adam)
 
     t0 = time.perf_counter()
-    run(1)  # warm-up (allocator, thread pool)
+    run(2)  # warm-up: 2 iterations (allocator, thread pool)
     t1 = time.perf_counter()
-    per = max(t1 - t0, 1e-3)
-    iters = int(max(2, min(200, budget_s / per)))
+    per = max((t1 - t0) / 2, 1e-3)
+    iters = int(max(5, min(200, budget_s / per)))
     t0 = time.perf_counter()
     run(iters)
     el = time.perf_counter() - t0
     N = X.shape[0]
     return {"value": N * iters / el, "unit": "samples/s", "cores": torch.get_num_threads(), "kind": "port",
-            "sample": f"oracle/cp_oracle.py fit_Adam (torch {torch.__version__} CPU, reference op order) on the "
-                      f"same {N} x {list(cfg['dims'])} X, {iters} timed iterations after 1 warm-up "
-                      f"({el:.1f} s); os.cpu_count()={os.cpu_count()}",
-            "ms_per_step": 1e3 * el / iters}
+            "sample": f"oracle/cp_oracle.py fit_Adam (torch {torch.__version__} CPU, the reference's op order) on "
+                      f"the same {N} x {list(cfg['dims'])} X (full per-GPU size), {iters} timed iterations after 2 "
+                      f"warm-up ({el:.1f} s), torch.set_num_threads({nthreads}) = every CPU in this process's "
+                      f"affinity",
+            "host": info, "ms_per_step": 1e3 * el / iters}
 
 
 def main():
@@ -142,6 +171,7 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--cpu-threads", type=int, default=None, help="CPU baseline threads (default: affinity size)")
     ap.add_argument("--time-all-kernels", action="store_true",
                     help="hipEvent-time every kernel kind (adds per-launch event overhead)")
     ap.add_argument("--traffic", default=os.path.join(HERE, "profiles", "traffic.json"),
@@ -238,6 +268,11 @@ def main():
     elif kt["stream_fused"][1]:
         dom = "stream_fused"
         bytes_launch = N * P * 4 + N * 4
+        if cfg.get("windowed"):
+            # overlapping windows: the unique series (N + L - 1) x F is what must cross HBM; the
+            # N * P window bytes are logical reads, mostly served by L2 / MALL
+            L, F = cfg["dims"][0], int(np.prod(cfg["dims"][1:]))
+            bytes_launch = (N + L - 1) * F * 4 + N * 4
         dom_name = "k_linear_cluster" if "cluster-1pass" in plan.describe else "k_linear_fused"
     else:
         dom = "stream_rows" if kt["stream_rows"][0] >= kt["stream_cols"][0] else "stream_cols"
@@ -248,6 +283,7 @@ def main():
     dom_ms = kernel_avg[dom]
     achieved = bytes_launch / (dom_ms * 1e-3) / 1e9
     traffic = None
+    traffic_src = None
     if os.path.exists(args.traffic):
         try:
             with open(args.traffic) as f:
@@ -255,6 +291,8 @@ def main():
             ent = tj.get(args.config, {}).get(dom_name)
             if ent:
                 traffic = ent.get("hbm_bytes_per_launch")
+                traffic_src = (f"read from {os.path.relpath(args.traffic, HERE)} (rocprofv3 FETCH_SIZE/WRITE_SIZE "
+                               f"passes of this kernel, {tj.get('round', 'earlier run')}), not measured in this run")
         except Exception:
             traffic = None
     iter_bytes = sum(N * P * 4 for _ in stream_kinds)
@@ -278,6 +316,7 @@ def main():
         "achieved_hbm_GBps_per_gpu": iter_bytes / (ms_step * 1e-3) / 1e9,
         "roofline": {"bound": "hbm", "kernel": dom_name, "achieved": achieved, "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
+                     "traffic_source": traffic_src,
                      "kernel_avg_ms": dom_ms, "algorithmic_bytes_per_launch": bytes_launch},
         "kernel_avg_ms": kernel_avg,
     }
@@ -287,13 +326,14 @@ def main():
         tflops = flops_launch / (dom_ms * 1e-3) / 1e12
         out["roofline"] = {"bound": "mfma", "kernel": dom_name, "achieved": tflops, "peak": FP32_MFMA_PEAK_TFLOPS,
                            "unit": "TFLOP/s", "frac": tflops / FP32_MFMA_PEAK_TFLOPS, "traffic": traffic,
+                           "traffic_source": traffic_src,
                            "kernel_avg_ms": dom_ms, "algorithmic_flops_per_launch": flops_launch,
                            "algorithmic_bytes_per_launch": bytes_launch, "hbm_GBps": achieved,
                            "hbm_frac": achieved / HBM_PEAK_GBPS}
         out["dtype"] = "fp32"
     if rank_id == 0 and world == 1 and not args.no_cpu_baseline:
         log("cpu baseline ...")
-        out["cpu_baseline"] = cpu_baseline(cfg, X, y, init, args.cpu_budget)
+        out["cpu_baseline"] = cpu_baseline(cfg, X, y, init, args.cpu_budget, args.cpu_threads)
     else:
         out["cpu_baseline"] = None
     if rank_id == 0:

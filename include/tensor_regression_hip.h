@@ -24,8 +24,10 @@
  *     list order, each factor (I_f x R) row-major, followed by the scalar bias for the
  *     linear model: [A_1 | A_2 | ... | A_F | (bias)].  tr_plan_factor_offset() gives the
  *     offsets; tr_plan_num_params() the total.
- *   - Gradient arena: same layout as the parameter arena plus ONE trailing slot holding the
- *     data loss, i.e. tr_plan_num_grads() = tr_plan_num_params() + 1.  Data-term gradients
+ *   - Gradient arena: same layout as the parameter arena plus TWO trailing slots: the data
+ *     loss, then the device status (0.0 = the pass succeeded; nonzero = a kernel of the pass
+ *     failed, see tr_plan_status), i.e. tr_plan_num_grads() = tr_plan_num_params() + 2.
+ *     Both slots survive the cross-shard sum meaningfully.  Data-term gradients
  *     are already normalised by the GLOBAL sample count (linear) or class-weight total
  *     (multinomial), so the element-wise sum of the arenas of disjoint sample shards is the
  *     full-data gradient — one all-reduce(sum) per iteration is the only exchange.
@@ -46,13 +48,18 @@
 extern "C" {
 #endif
 
-#define TR_ABI_VERSION 5
+#define TR_ABI_VERSION 6
 
 #define TR_MODEL_LINEAR 0      /* CP_linear_regression: y_hat = <X, [[w; Phi]]> + bias, MSE */
 #define TR_MODEL_MULTINOMIAL 1 /* CP_logistic_regression: softmax(<X, [[w; Phi]]>), CE(weight) */
 #define TR_MODEL_SPECTRAL 2    /* spectral CP_linear_regression: lin_model + stepwise_spectral_model, MSE */
 
 #define TR_MAX_FACTORS 8
+
+/* *stop_flag written by tr_adam_step when the gradient arena's status slot is set: the step was
+ * NOT applied, parameters and Adam state are those after iteration `iter - 1`.
+ * Value = TR_STOP_DEVICE_ERROR - iter (plateau stops are > 0, spectral NaN stops > -2^30). */
+#define TR_STOP_DEVICE_ERROR (-(1 << 30))
 
 #define TR_E_ARG (-1)      /* invalid argument (shape/size/pointer) */
 #define TR_E_UNSUPPORTED (-2)
@@ -62,6 +69,11 @@ typedef struct tr_plan tr_plan;
 
 /* Library ABI version (TR_ABI_VERSION). */
 int tr_abi_version(void);
+
+/* SHA-256 (hex) of the sources the library was compiled from (the .hip and .h files of csrc,
+ * in byte order of their names, then this header); the Python loader refuses a library whose id
+ * does not match the sources next to it. */
+const char* tr_build_id(void);
 
 /* Thread-local message describing the most recent failure ("" if none). */
 const char* tr_last_error(void);
@@ -88,7 +100,7 @@ int tr_plan_create(tr_plan** out, int device, int model, int n_feature_modes,
 int tr_plan_destroy(tr_plan* plan);
 
 int64_t tr_plan_num_params(const tr_plan* plan); /* factors (+ bias) */
-int64_t tr_plan_num_grads(const tr_plan* plan);  /* num_params + 1 (data-loss slot) */
+int64_t tr_plan_num_grads(const tr_plan* plan);  /* num_params + 2 (data-loss + status slots) */
 int64_t tr_plan_factor_offset(const tr_plan* plan, int factor);
 int64_t tr_plan_workspace_bytes(const tr_plan* plan);
 /* Human-readable description of the kernel strategy chosen for this plan (host string). */
@@ -109,11 +121,19 @@ int tr_plan_set_x_stride(tr_plan* plan, int64_t stride);
  * Device status of the plan's kernels since the last call (synchronises the device).
  * *status = 0: healthy.  Bit 0: a cross-workgroup exchange of the single-pass kernel for wide
  * rows (P beyond one CU's LDS) gave up waiting for a partner workgroup — it happens only when
- * the GPU is shared with another kernel so the cluster was not co-resident; that call's
- * gradient and loss are NaN.  No reference counterpart (the reference has no device kernels);
- * fit loops call it at their host synchronisation points and raise.
+ * the GPU is shared with another kernel so the cluster was not co-resident (the plan launches at
+ * most one workgroup per CU, so an unshared GPU always holds the whole grid); that call's
+ * gradient and loss are NaN and the gradient arena's status slot is set.  No reference
+ * counterpart (the reference has no device kernels).
  */
 int tr_plan_status(tr_plan* plan, int32_t* status);
+
+/*
+ * Recover from a device-side failure (status bit set / TR_STOP_DEVICE_ERROR): clears the status
+ * and switches the plan to its two-pass path, which has no cross-workgroup dependence.  The fit
+ * loop then resumes at the failed iteration from the untouched parameters and Adam state.
+ */
+int tr_plan_recover(tr_plan* plan);
 
 /*
  * Forward model only (predict path).

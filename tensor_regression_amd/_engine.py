@@ -7,9 +7,12 @@ per-iteration `loss.item()` host sync (standard_tensor_regression.py:464) is rep
 device loss history plus a device stop flag (the plateau test of :467-470 runs on the GPU), so
 the host enqueues `sync_every` iterations between synchronisations.
 """
+import atexit
 import ctypes
 import math
 import os
+import sys
+import weakref
 
 import numpy as np
 import torch
@@ -20,6 +23,9 @@ from ._lib import check, ptr
 _DEFAULT_SOFTPLUS = {"beta": 50, "threshold": 1}
 # fit_Adam: fold the next iteration's factor preparation into each Adam step (tests toggle it)
 _PREPARE_NEXT = os.environ.get("TR_NO_PREPARE_NEXT", "0") in ("", "0")
+# a pass that failed on the device (wide-row cluster exchange timed out: GPU shared): "fallback"
+# resumes the fit on the two-pass path from the untouched state; "raise" raises RuntimeError
+_ON_DEVICE_ERROR = os.environ.get("TR_ON_DEVICE_ERROR", "fallback")
 # torch.optim.Adam defaults (torch/optim/adam.py)
 _ADAM_DEFAULTS = dict(lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0, amsgrad=False,
                       foreach=None, maximize=False, capturable=False, differentiable=False,
@@ -30,6 +36,14 @@ def softplus_params(softplus_kwargs):
     kw = _DEFAULT_SOFTPLUS if softplus_kwargs is None else softplus_kwargs
     # torch.nn.functional.softplus defaults when a key is absent
     return float(kw.get("beta", 1.0)), float(kw.get("threshold", 20.0))
+
+
+def nonlin_key(non_negative, softplus_kwargs, n_factors):
+    """The per-factor softplus switches and (beta, threshold) a plan is built with: the reference
+    reads self.non_negative / self.softplus_kwargs on every call, so a plan whose key differs from
+    the model's current one must be rebuilt."""
+    nn = tuple(1 if bool(non_negative[f]) else 0 for f in range(n_factors))
+    return (nn,) + softplus_params(softplus_kwargs)
 
 
 def adam_hparams(Adam_kwargs):
@@ -85,6 +99,32 @@ def compute_device(X, model_device):
     return torch.cuda.current_device()
 
 
+_live_plans = weakref.WeakSet()
+_atexit_registered = False
+
+
+def _track(plan):
+    """Remember a live plan; the first one registers the exit hook.  Registered after torch has
+    initialised HIP, so (atexit is LIFO) it runs before torch's and the HIP runtime's own teardown."""
+    global _atexit_registered
+    _live_plans.add(plan)
+    if not _atexit_registered:
+        atexit.register(_destroy_all_plans)
+        _atexit_registered = True
+
+
+def _destroy_all_plans():
+    """Free every plan's workspace and timing events while the HIP runtime is still fully alive.
+    Plans held by module-level caches would otherwise be destroyed during interpreter teardown,
+    after a profiler's tool finalisation or the runtime's static destructors (the exit-time SIGSEGV
+    seen under rocprofv3)."""
+    for plan in list(_live_plans):
+        try:
+            plan.destroy()
+        except Exception:
+            pass
+
+
 def stream_handle(dev):
     return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
 
@@ -104,8 +144,8 @@ class Plan:
         self.max_rows = int(max_rows)
         nf = len(self.feature_dims) + (1 if model == _lib.TR_MODEL_MULTINOMIAL else 0)
         self.n_factors = nf
-        nn = [1 if bool(non_negative[f]) else 0 for f in range(nf)]
-        beta, thr = softplus_params(softplus_kwargs)
+        self.nonlin = nonlin_key(non_negative, softplus_kwargs, nf)
+        nn, beta, thr = self.nonlin
         dims = (ctypes.c_int64 * len(self.feature_dims))(*self.feature_dims)
         nna = (ctypes.c_int32 * nf)(*nn)
         h = ctypes.c_void_p()
@@ -114,19 +154,28 @@ class Plan:
                                          self.n_classes, self.rank, max(1, self.max_rows), nna, beta, thr)
         check(rc, "tr_plan_create")
         self.h = h
+        _track(self)
         self.num_params = int(self.lib.tr_plan_num_params(h))
         self.num_grads = int(self.lib.tr_plan_num_grads(h))
         self.offsets = [int(self.lib.tr_plan_factor_offset(h, f)) for f in range(nf + 1)]
         self.describe = self.lib.tr_plan_describe(h).decode()
 
-    def __del__(self):
+    def destroy(self):
+        """Release the C plan (idempotent).  tr_plan_destroy synchronises the plan's device first."""
         h = getattr(self, "h", None)
         if h is not None and h.value:
-            try:
-                self.lib.tr_plan_destroy(h)
-            except Exception:
-                pass
             self.h = None
+            self.lib.tr_plan_destroy(h)
+
+    def __del__(self):
+        # during interpreter shutdown the exit hook has already destroyed every plan; never call
+        # into HIP from a finaliser that may run after the runtime is gone
+        if sys.is_finalizing():
+            return
+        try:
+            self.destroy()
+        except Exception:
+            pass
 
     # ---- parameter arena -------------------------------------------------------------------
     def factor_shapes(self):
@@ -191,6 +240,31 @@ class Plan:
             raise RuntimeError(f"gfx950 kernel status {st.value:#x}: a cross-workgroup exchange timed out "
                                "(the GPU was shared with another kernel); the affected gradients are NaN")
 
+    @property
+    def may_fail_on_device(self):
+        """Only the wide-row cluster pass depends on co-resident workgroups."""
+        return "cluster-1pass" in self.describe and "recovered=2pass" not in self.describe
+
+    def recover(self, where):
+        """After a failed pass: two-pass from now on (tr_plan_recover), or raise (TR_ON_DEVICE_ERROR=raise)."""
+        if _ON_DEVICE_ERROR == "raise":
+            raise RuntimeError(f"gfx950 single-pass kernel failed on the device ({where}): a cross-workgroup "
+                               "exchange timed out (the GPU was shared with another kernel); no step was applied")
+        import warnings
+        warnings.warn(f"gfx950 wide-row single pass failed on the device ({where}; GPU shared?): continuing on "
+                      "the two-pass path from the last good iteration", RuntimeWarning, stacklevel=3)
+        check(self.lib.tr_plan_recover(self.h), "tr_plan_recover")
+        self.describe = self.lib.tr_plan_describe(self.h).decode()
+
+    def loss_grad_checked(self, X, target, class_weight, norm, arena, weights, grad):
+        """loss_grad for callers outside the Adam loop (LBFGS closures, one-off evaluations): on a
+        plan whose pass can fail on the device, check the status slot and redo the pass on the
+        two-pass path if it failed (one host sync, only on such plans)."""
+        self.loss_grad(X, target, class_weight, norm, arena, weights, grad)
+        if self.may_fail_on_device and float(grad[self.num_params + 1].item()) != 0.0:
+            self.recover("loss_grad")
+            self.loss_grad(X, target, class_weight, norm, arena, weights, grad)
+
     # ---- entry points ------------------------------------------------------------------------
     def _set_stride(self, X):
         """Tell the plan X's row stride (windowed / strided views) when it changes."""
@@ -247,8 +321,9 @@ class SpectralPlan(Plan):
         self.rank_normal, self.rank_spectral, self.n_complex = int(rank_normal), int(rank_spectral), int(n_complex)
         self.max_rows = int(max_rows)
         self.n_factors = 6
-        nn = (ctypes.c_int32 * 3)(*[1 if bool(non_negative[f]) else 0 for f in range(3)])
-        beta, thr = softplus_params(softplus_kwargs)
+        self.nonlin = nonlin_key(non_negative, softplus_kwargs, 3)
+        nn = (ctypes.c_int32 * 3)(*self.nonlin[0])
+        beta, thr = self.nonlin[1:]
         h = ctypes.c_void_p()
         with torch.cuda.device(self.dev):
             rc = self.lib.tr_plan_create_spectral(ctypes.byref(h), self.dev, self.dims[0], self.dims[1], self.dims[2],
@@ -256,6 +331,7 @@ class SpectralPlan(Plan):
                                                   max(1, self.max_rows), nn, beta, thr)
         check(rc, "tr_plan_create_spectral")
         self.h = h
+        _track(self)
         self.num_params = int(self.lib.tr_plan_num_params(h))
         self.num_grads = int(self.lib.tr_plan_num_grads(h))
         self.offsets = [int(self.lib.tr_plan_factor_offset(h, f)) for f in range(7)]
@@ -361,15 +437,50 @@ def loss_grad_any(plan, X, target, class_weight, norm, arena, weights, grad, sto
             grad.add_(tmp)
 
 
+def check_uniform(value, process_group, what, device):
+    """Raise ValueError on EVERY rank when the ranks disagree on an integer (one all-reduce), so a
+    mismatch cannot leave some ranks blocked in a later collective."""
+    import torch.distributed as dist
+    n = torch.tensor([int(value), -int(value)], dtype=torch.int64, device=device)
+    dist.all_reduce(n, op=dist.ReduceOp.MAX, group=process_group)
+    if int(n[0]) != int(value) or -int(n[1]) != int(value):
+        raise ValueError(f"ranks disagree on {what} (this rank {int(value)}, max {int(n[0])}, min {-int(n[1])}); "
+                         "a multinomial model's class count comes from its local labels: build every rank's model "
+                         "with the global class count (Bcp_init of the global shapes)")
+
+
+def sync_replicas(arena, process_group):
+    """Start every rank's replica from the same parameters (multi-GPU fit_Adam).
+
+    The ranks must agree on the arena layout (for the multinomial model: the number of classes,
+    taken by the constructor from the local labels) — checked with one MIN/MAX all-reduce so a
+    mismatch raises on every rank instead of hanging in the per-iteration all-reduce — and then
+    take group rank 0's parameters (one broadcast per fit).  From there the replicas stay in
+    lock-step: every rank applies the identical step to the bitwise-identical all-reduced sums."""
+    import torch.distributed as dist
+    check_uniform(arena.numel(), process_group, "the parameter arena size", arena.device)
+    src = dist.get_global_rank(process_group, 0) if process_group is not None else 0
+    dist.broadcast(arena, src=src, group=process_group)
+
+
 def run_adam_fit(plan, X, target, class_weight, norm, arena, weights, lambda_L2, max_iter, tol, patience,
-                 hp, loss_running, verbose_cb=None, allreduce=None, sync_every=64):
+                 hp, loss_running, verbose_cb=None, process_group=None, sync_every=64):
     """The fit_Adam loop (standard…py:453-470 / multinomial…py:447-465), device resident.
 
     Returns (convergence_reached, number_of_iterations_run).  `loss_running` is extended in place
-    with the reference's per-iteration losses.  `allreduce(grad)` (optional) sums the gradient
-    arena over sample shards between the local gradient and the Adam step.
+    with the reference's per-iteration losses.  With a `process_group` (torch.distributed; RCCL
+    on the GPU) X / target are this rank's sample shard: the replicas start from group rank 0's
+    parameters (sync_replicas) and one all-reduce(sum) of the gradient arena — data gradients,
+    data loss and the device status slot — runs between the local gradient and the Adam step.
     """
     dev = plan.device_str
+    allreduce = None
+    if process_group is not None:
+        import torch.distributed as dist
+        sync_replicas(arena, process_group)
+
+        def allreduce(g):
+            dist.all_reduce(g, group=process_group)
     opts = dict(dtype=torch.float32, device=dev)
     grad = torch.zeros(plan.num_grads, **opts)
     m = torch.zeros(plan.num_params, **opts)
@@ -418,6 +529,15 @@ def _adam_loop(plan, X, target, class_weight, norm, arena, weights, lambda_L2, m
             plan.adam_step(arena, grad, m, v, vmax, lambda_L2, hp, it + 1, hist, base, it, patience, tol, stop)
         ii += n
         stopped_at = int(stop.item())  # one host sync per chunk
+        if stopped_at <= _lib.TR_STOP_DEVICE_ERROR:
+            # a pass failed on the device (on any rank: the status slot is all-reduced with the
+            # gradients, so every rank stops at the same iteration): nothing from that iteration on
+            # was applied, so resume it on the two-pass path with the same parameters / Adam state
+            failed = _lib.TR_STOP_DEVICE_ERROR - stopped_at
+            plan.recover(f"iteration {failed}")
+            stop.zero_()
+            ii, stopped_at = failed, 0
+            continue
         plan.check_status()
         if verbose_cb is not None:
             verbose_cb.after_step(ii - 1, float(hist[base + ii - 1].item()))

@@ -6,13 +6,15 @@ is missing or fails to load, every product entry point raises, so a test or benc
 never silently run on a CPU / eager-PyTorch path.
 """
 import ctypes
+import hashlib
 import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TR_HIP_LIB", os.path.join(_HERE, "libtr_hip.so"))
 
-TR_ABI_VERSION = 5
+TR_ABI_VERSION = 6
+TR_STOP_DEVICE_ERROR = -(1 << 30)
 TR_MODEL_LINEAR = 0
 TR_MODEL_MULTINOMIAL = 1
 TR_MODEL_SPECTRAL = 2
@@ -25,6 +27,8 @@ _vp = _c.c_void_p
 SIGNATURES = {
     "tr_abi_version": (_c.c_int, []),
     "tr_last_error": (_c.c_char_p, []),
+    "tr_build_id": (_c.c_char_p, []),
+    "tr_plan_recover": (_c.c_int, [_vp]),
     "tr_plan_create": (_c.c_int, [_c.POINTER(_vp), _c.c_int, _c.c_int, _c.c_int, _c.POINTER(_c.c_int64),
                                   _c.c_int, _c.c_int, _c.c_int64, _c.POINTER(_c.c_int32), _c.c_float,
                                   _c.c_float]),
@@ -59,6 +63,22 @@ class HipLibraryError(RuntimeError):
     """The gfx950 extension is missing, stale, or a call into it failed."""
 
 
+def source_build_id():
+    """sha256 of the sources next to the package, exactly as the Makefile's build/tr_build_id.h
+    computes it (csrc/*.hip and csrc/*.h in byte order of their names, then the public header);
+    None when the sources are not shipped."""
+    csrc = os.path.join(_HERE, "csrc")
+    header = os.path.join(os.path.dirname(_HERE), "include", "tensor_regression_hip.h")
+    if not os.path.isdir(csrc) or not os.path.exists(header):
+        return None
+    names = sorted(n for n in os.listdir(csrc) if n.endswith((".hip", ".h")))
+    h = hashlib.sha256()
+    for path in [os.path.join(csrc, n) for n in names] + [header]:
+        with open(path, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
 def load():
     """Load (once) and return the ctypes library; raises HipLibraryError if unavailable."""
     global _lib
@@ -80,6 +100,11 @@ def load():
         v = lib.tr_abi_version()
         if v != TR_ABI_VERSION:
             raise HipLibraryError(f"{LIB_PATH} has ABI version {v}, expected {TR_ABI_VERSION}; rebuild it")
+        want = source_build_id()
+        got = (lib.tr_build_id() or b"").decode()
+        if want is not None and got != want and os.environ.get("TR_HIP_LIB") is None:
+            raise HipLibraryError(f"{LIB_PATH} was built from other sources (build id {got[:12]}, sources "
+                                  f"{want[:12]}); rebuild it with `make -C tensor_regression_amd/csrc`")
         _lib = lib
         return lib
 

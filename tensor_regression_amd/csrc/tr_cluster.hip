@@ -17,10 +17,15 @@
 // so its granule polls do not queue behind a row of vmcnt-counted X loads; the hop overlaps the
 // next row's HBM transfer.
 //
-// Safety: a spin that sees no partner for ~2^16 polls (a member not resident, e.g. the GPU
-// shared with another kernel) sets *err, marks the workgroup dead (NaN partials from then on) and
-// runs to completion; the host reads *err through tr_plan_status.  Tags grow monotonically per
-// plan (host-side counter), so granules left by earlier launches never match.
+// Co-residency: the plan launches S * floor(ncu / S) <= ncu workgroups of one workgroup per CU
+// (occupancy >= 1 checked at plan time), so on an unshared GPU every member is resident.
+// Safety when it is not: a spin that sees no partner for err[1] polls (2^16 by default; the plan
+// takes TR_CLUSTER_SPIN_LIMIT for tests) sets err[0], marks the workgroup dead (NaN partials from
+// then on) and runs to completion.  k_reduce_slabs copies err[0] into the gradient arena's status
+// slot, where k_update sees it on every rank after the all-reduce: it stops the fit before
+// applying the step, and the host falls back to the two-pass path from the untouched
+// parameters.  Tags grow monotonically per plan (host-side counter), so granules left by earlier
+// launches never match.
 #include "tr_common.h"
 #include "tr_kernels.h"
 
@@ -30,7 +35,6 @@ namespace {
 constexpr int CL_T = 512;               // threads per workgroup
 constexpr int CL_NW = CL_T / TR_WAVE;   // 8 waves
 constexpr int CL_TC = CL_T - TR_WAVE;   // 448 streaming threads (waves 1..7)
-constexpr int CL_SPIN_LIMIT = 1 << 16;  // bounded poll (see header)
 
 __device__ __forceinline__ void cl_barrier() {
   // LDS-only barrier: the streaming waves' next-row X loads stay in flight across it.
@@ -84,6 +88,7 @@ __global__ __launch_bounds__(CL_T) void k_linear_cluster(
   for (int c = 0; c < CH; ++c) g[c] = make_float4(0.f, 0.f, 0.f, 0.f);
   double sse = 0.0, rsum = 0.0;
   bool dead = false;
+  const int spin_limit = (int)err[1];  // bounded poll (see header)
 
   auto row_of = [&](int64_t i) -> int64_t { return reverse ? (r1 - 1 - i) : (r0 + i); };
   auto load = [&](float4(&x)[CH], int64_t i) {
@@ -123,6 +128,10 @@ __global__ __launch_bounds__(CL_T) void k_linear_cluster(
         __hip_atomic_store(slot + s, ((unsigned long long)tag << 32) | (unsigned long long)__float_as_uint(part),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       float v = lane == s ? part : 0.f;
+      if (!dead && spin_limit == 0) {  // test knob (TR_CLUSTER_SPIN_LIMIT=0): every exchange fails
+        dead = true;
+        if (lane == 0) atomicOr(err, 1u);
+      }
       if (!dead) {
         for (int spins = 0;; ++spins) {
           bool ok = true;
@@ -132,7 +141,7 @@ __global__ __launch_bounds__(CL_T) void k_linear_cluster(
             v = __uint_as_float((uint32_t)x);
           }
           if (__all(ok)) break;
-          if (spins >= CL_SPIN_LIMIT) {
+          if (spins >= spin_limit) {
             dead = true;
             if (lane == 0) atomicOr(err, 1u);
             break;

@@ -7,6 +7,10 @@
 #define TR_WAVE 64
 #define TR_MAXF 8     // max factors (modes of the dense coefficient tensor)
 #define TR_MAXR 64    // max CP rank
+// stop-flag value written by k_update when the pass it was about to apply failed on the device
+// (gradient-arena status slot set): TR_STOP_DEVICE_ERROR - iteration.  Distinct from the plateau
+// stop (iterations completed, > 0) and the spectral NaN stop (-(iterations run) > -2^30).
+#define TR_STOP_DEVICE_ERROR (-(1 << 30))
 
 // Description of the dense coefficient tensor B and its Kruskal factors, passed by value.
 //

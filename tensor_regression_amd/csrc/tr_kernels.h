@@ -84,7 +84,8 @@ hipError_t launch_cols(int C, int W, int64_t nstripes, int64_t nchunks, const fl
 hipError_t launch_reduce_slabs(int W, const float* part, int64_t nslabs, int64_t ncols, float* out,
                                const double* dpart, int64_t nd, double loss_scale, float* loss_slot,
                                float* bias_slot, const int32_t* stop, hipStream_t st,
-                               const float* chain_dphi = nullptr, float* chain_out = nullptr, int64_t nchain = 0);
+                               const float* chain_dphi = nullptr, float* chain_out = nullptr, int64_t nchain = 0,
+                               const uint32_t* err = nullptr);
 hipError_t launch_mttkrp(const FactorSet& fs, const float* phi, const float* dphi, const float* w,
                          const float* G, float* grad, const int32_t* stop, hipStream_t st);
 hipError_t launch_update(const FactorSet& fs, int n_bias, float* params, const float* grad,

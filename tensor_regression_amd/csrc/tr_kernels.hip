@@ -673,6 +673,7 @@ __global__ __launch_bounds__(1024) void k_reduce_slabs(const float* __restrict__
                                                        float* __restrict__ bias_slot,
                                                        const float* __restrict__ chain_dphi,
                                                        float* __restrict__ chain_out, int64_t nchain,
+                                                       const uint32_t* __restrict__ err,
                                                        const int32_t* __restrict__ stop) {
   using V = VecT<W>;
   using VT = typename V::T;
@@ -739,6 +740,9 @@ __global__ __launch_bounds__(1024) void k_reduce_slabs(const float* __restrict__
       if (bias_slot != nullptr) *bias_slot = (float)b;
     }
   }
+  // device status slot (after the loss slot): nonzero iff a kernel of this pass failed
+  if (blockIdx.x == 0 && threadIdx.x == 0 && loss_slot != nullptr)
+    loss_slot[1] = (err != nullptr && err[0] != 0u) ? 1.0f : 0.0f;
 }
 
 // ==========================================================================================
@@ -975,6 +979,12 @@ __global__ __launch_bounds__(1024) void k_update(FactorSet fs, int n_bias, float
   const int lane = t & (TR_WAVE - 1);
   const int q = t / TR_WAVE;
   const int NWV = blockDim.x / TR_WAVE;
+  // a failed pass (status slot set, summed over shards by the all-reduce): stop the fit before
+  // the step so the parameters and the Adam state stay those of the last good iteration
+  if (ua.mode == 0 && stop != nullptr && grad[fs.nfelem + n_bias + 1] != 0.0f) {
+    if (t == 0) *stop = TR_STOP_DEVICE_ERROR - (int32_t)ua.iter;
+    return;
+  }
   // ||A_f||_F of every factor (raw parameters) in one pass; fixed-order block reduction
   {
     float accn[TR_MAXF];
@@ -1261,14 +1271,14 @@ hipError_t launch_cols(int C, int W, int64_t nstripes, int64_t nchunks, const fl
 hipError_t launch_reduce_slabs(int W, const float* part, int64_t nslabs, int64_t ncols, float* out,
                                const double* dpart, int64_t nd, double loss_scale, float* loss_slot,
                                float* bias_slot, const int32_t* stop, hipStream_t st, const float* chain_dphi,
-                               float* chain_out, int64_t nchain) {
+                               float* chain_out, int64_t nchain, const uint32_t* err) {
   const unsigned grid = cdiv(ncols / W, TR_WAVE);
   if (W == 4)
     hipLaunchKernelGGL(k_reduce_slabs<4>, dim3(grid), dim3(1024), 0, st, part, nslabs, ncols, out, dpart, nd,
-                       loss_scale, loss_slot, bias_slot, chain_dphi, chain_out, nchain, stop);
+                       loss_scale, loss_slot, bias_slot, chain_dphi, chain_out, nchain, err, stop);
   else
     hipLaunchKernelGGL(k_reduce_slabs<1>, dim3(grid), dim3(1024), 0, st, part, nslabs, ncols, out, dpart, nd,
-                       loss_scale, loss_slot, bias_slot, chain_dphi, chain_out, nchain, stop);
+                       loss_scale, loss_slot, bias_slot, chain_dphi, chain_out, nchain, err, stop);
   return hipGetLastError();
 }
 

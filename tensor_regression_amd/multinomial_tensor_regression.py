@@ -144,7 +144,9 @@ class CP_logistic_regression():
                              f"tensor_1.shape={list(Xd.shape)}, factors={[tuple(A.shape) for A in self.Bcp]}")
         C, R = int(self.Bcp[-1].shape[0]), int(self.Bcp[0].shape[1])
         p = self._plan
-        if p is None or p.max_rows < rows or p.feature_dims != dims or p.n_classes != C or p.rank != R:
+        if (p is None or p.max_rows < rows or p.feature_dims != dims or p.n_classes != C or p.rank != R
+                or p.dev != _engine.device_index(Xd.device)
+                or p.nonlin != _engine.nonlin_key(self.non_negative, self.softplus_kwargs, len(dims) + 1)):
             p = Plan(_lib.TR_MODEL_MULTINOMIAL, dims, C, R, rows, self.non_negative, self.softplus_kwargs,
                      Xd.device)
             self._plan = p
@@ -192,7 +194,7 @@ class CP_logistic_regression():
             if ii % running_loss_logging_interval == 0:
                 arena = plan.pack(self.Bcp)
                 plan.loss_grad(Xd, yd, cw, W, arena, w, grad)  # data loss only (reference :372)
-                self.loss_running.append(float(grad[-1].item()))
+                self.loss_running.append(float(grad[plan.num_params].item()))
                 if verbose == 2:
                     print(f'Iteration: {ii}, Loss: {self.loss_running[-1]}')
             if ii > patience:
@@ -214,18 +216,14 @@ class CP_logistic_regression():
         hp = adam_hparams(Adam_kwargs)
         dev, Xd, yd = self._device_data()
         plan = self._get_plan(Xd, Xd.shape[0])
-        cw, W = self._class_weights(weights, dev, yd, process_group)
-        allreduce = None
         if process_group is not None:
-            import torch.distributed as dist
-
-            def allreduce(g):
-                dist.all_reduce(g, group=process_group)
+            _engine.check_uniform(int(self.Bcp[-1].shape[0]), process_group, "the number of classes", Xd.device)
+        cw, W = self._class_weights(weights, dev, yd, process_group)
         arena = plan.pack(self.Bcp)
         w = self.weights.to(f"cuda:{dev}", torch.float32).contiguous()
         vcb = _Verbose() if verbose == 2 else None
         convergence_reached, _ = run_adam_fit(plan, Xd, yd, cw, W, arena, w, lambda_L2, max_iter, tol, patience,
-                                              hp, self.loss_running, verbose_cb=vcb, allreduce=allreduce)
+                                              hp, self.loss_running, verbose_cb=vcb, process_group=process_group)
         plan.unpack_into(arena, self.Bcp)
         if (verbose is True) or (verbose >= 1):
             print('Convergence reached' if convergence_reached else

@@ -263,10 +263,11 @@ class CP_linear_regression():
         if len(X.shape) != 3 or (int(X.shape[1]), int(X.shape[2])) != (W, D):
             raise ValueError(f"X must be (N, {W}, {D}) for these factors; got {tuple(X.shape)}")
         p = self._plan
+        dev = _engine.device_index(X.device if isinstance(X, torch.Tensor) else f"cuda:{X.dev_index}")
         if (p is None or p.max_rows < rows or p.dims != (W, D, O)
-                or (p.rank_normal, p.rank_spectral, p.n_complex) != (Rn, Rs, Cc)):
-            p = SpectralPlan(W, D, O, Rn, Rs, Cc, rows, self.non_negative, self.softplus_kwargs,
-                             X.device if isinstance(X, torch.Tensor) else X.dev_index)
+                or (p.rank_normal, p.rank_spectral, p.n_complex) != (Rn, Rs, Cc) or p.dev != dev
+                or p.nonlin != _engine.nonlin_key(self.non_negative, self.softplus_kwargs, 3)):
+            p = SpectralPlan(W, D, O, Rn, Rs, Cc, rows, self.non_negative, self.softplus_kwargs, f"cuda:{dev}")
             self._plan = p
         return p
 
@@ -367,15 +368,11 @@ class CP_linear_regression():
         X, y, dev = self._inputs(X, y)
         plan = self._get_plan(X, X.shape[0])
         n_global = float(X.shape[0])
-        allreduce = None
         if process_group is not None:
             import torch.distributed as dist
             n_t = torch.tensor([X.shape[0]], dtype=torch.float64, device=f"cuda:{dev}")
             dist.all_reduce(n_t, group=process_group)
             n_global = float(n_t.item())
-
-            def allreduce(g):
-                dist.all_reduce(g, group=process_group)
         norm = n_global * y.shape[1]
         arena = self._arena(plan)
         w = self._weights(dev)
@@ -384,7 +381,7 @@ class CP_linear_regression():
             raise NotImplementedError("verbose=2/3 (per-iteration y_hat variance) is not offered for a HostStream X")
         vcb = _VerbosePrinter(plan, X, y, w, norm) if verbose in (2, 3) else None
         convergence_reached, _ = run_adam_fit(plan, X, y, None, norm, arena, w, lambda_L2, max_iter, tol, patience,
-                                              hp, self.loss_running, verbose_cb=vcb, allreduce=allreduce)
+                                              hp, self.loss_running, verbose_cb=vcb, process_group=process_group)
         plan.unpack_into(arena, self.Bcp_n, self.Bcp_c, self.bias)
         if plan.last_stop < 0:
             print('Loss is NaN. Stopping.')

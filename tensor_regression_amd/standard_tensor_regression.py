@@ -186,9 +186,11 @@ class CP_linear_regression():
             raise ValueError(f"Incorrect shapes for inner product along {len(dims)} common modes. "
                              f"tensor_1.shape={list(X.shape)}, factors={[tuple(A.shape) for A in self.Bcp]}")
         p = self._plan
-        if p is None or p.max_rows < rows or p.feature_dims != dims or p.rank != int(self.Bcp[0].shape[1]):
+        dev = _engine.device_index(X.device if isinstance(X, torch.Tensor) else f"cuda:{X.dev_index}")
+        if (p is None or p.max_rows < rows or p.feature_dims != dims or p.rank != int(self.Bcp[0].shape[1])
+                or p.dev != dev or p.nonlin != _engine.nonlin_key(self.non_negative, self.softplus_kwargs, len(dims))):
             p = Plan(_lib.TR_MODEL_LINEAR, dims, 1, int(self.Bcp[0].shape[1]), rows, self.non_negative,
-                     self.softplus_kwargs, X.device if isinstance(X, torch.Tensor) else X.dev_index)
+                     self.softplus_kwargs, f"cuda:{dev}")
             self._plan = p
         return p
 
@@ -234,7 +236,7 @@ class CP_linear_regression():
         def closure():
             optimizer.zero_grad()
             arena = plan.pack(self.Bcp, self.bias)
-            plan.loss_grad(X, y, None, float(N), arena, w, grad)
+            plan.loss_grad_checked(X, y, None, float(N), arena, w, grad)
             plan.finalize_grad(arena, grad, lambda_L2, gtot, loss_out)
             views = plan.factor_views(gtot)
             for A, g in zip(self.Bcp, views):
@@ -278,21 +280,17 @@ class CP_linear_regression():
         from .util import HostStream
         if verbose == 2 and isinstance(X, HostStream):
             raise NotImplementedError("verbose=2 (per-iteration y_hat variance) is not offered for a HostStream X")
-        allreduce = None
         if process_group is not None:
             import torch.distributed as dist
             n_t = torch.tensor([X.shape[0]], dtype=torch.float64, device=f"cuda:{dev}")
             dist.all_reduce(n_t, group=process_group)
             n_global = float(n_t.item())
-
-            def allreduce(g):
-                dist.all_reduce(g, group=process_group)
         arena = plan.pack(self.Bcp, self.bias)
         w = self.weights.to(f"cuda:{dev}", torch.float32).contiguous()
         vcb = _VerbosePrinter(plan, X, y, w) if verbose == 2 else None
         convergence_reached, _ = run_adam_fit(plan, X, y, None, n_global, arena, w, lambda_L2, max_iter, tol,
                                               patience, hp, self.loss_running, verbose_cb=vcb,
-                                              allreduce=allreduce)
+                                              process_group=process_group)
         plan.unpack_into(arena, self.Bcp, self.bias)
         if (verbose is True) or (verbose >= 1):
             print('Convergence reached' if convergence_reached else

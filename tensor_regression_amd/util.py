@@ -1,102 +1,39 @@
-"""Data utilities — drop-in for the reference's `util.py` (kimerein/tensor_regression), plus the
-MI355X-native windowed view the gfx950 kernels read without materialising windows.
+"""Windowed and out-of-core sample sources for the gfx950 fit path.
 
-Reference surface kept (util.py:15-114): `set_device`, `squeeze_integers`, `WindowedDataset`,
-`make_WindowedDataloader` (torch Dataset / DataLoader over an untiled (T, ...) series; sample
-`idx` is the window `X[idx + win_range[0] : idx + win_range[1]]` with target `y[idx]`).
+The reference feeds windowed data through `util.WindowedDataset` (util.py:67-98): sample `idx`
+is the window `X_untiled[idx + w0 : idx + w1]` with target `y[idx]`, for `idx` in
+`usable_idx = arange(-w0, T - w1 + 1)`; its batch fits (standard_tensor_regression.py:478-620,
+commented out) stack such windows into a dense (N, w1 - w0, ...) X.  Here the same samples
+never get materialised:
 
-New: `windowed_view(X_untiled, y, win_range)` returns the SAME samples the dataset yields for
-`idx` in `dataset.usable_idx`, as an overlapping strided tensor view
-(N_windows, win_len, *feature_dims) with stride (F, F, ...) along the window axis — no copy, so
-X stays T x F in HBM instead of N x win_len x F.  The fit/predict entry points accept such views
-(`tr_plan_set_x_stride`): every kernel reads sample n at X + n*F.
+* `windowed_view(X_untiled, y, win_range)` — every usable window, in `usable_idx` order, as one
+  overlapping strided view (N, L, *F) with stride F along the sample axis.  X stays T x F in
+  HBM; each kernel reads sample n at X + n*F (`tr_plan_set_x_stride`).
+* `WindowedDataset` — the reference's indexing surface (`usable_idx`, `ds[idx]`) over that view.
+* `HostStream` — an X kept in pinned host memory and streamed through two device buffers per
+  iteration, for an X larger than the HBM one wants to spend.
+
+The reference's general helpers (`set_device`, `squeeze_integers`, `make_WindowedDataloader`'s
+random minibatching) are not on the fit path and are not provided.
 """
-import copy
-
 import numpy as np
 import torch
-from torch.utils.data import DataLoader, Dataset
 
-__all__ = ["set_device", "squeeze_integers", "WindowedDataset", "make_WindowedDataloader", "windowed_view",
-           "HostStream"]
+__all__ = ["windowed_view", "WindowedDataset", "HostStream"]
 
 
-def set_device(use_GPU=True, verbose=True):
-    """'cuda' if a HIP device is available and requested, else 'cpu' (util.py:15-35)."""
-    if use_GPU:
-        device = "cuda" if torch.cuda.is_available() else "cpu"
-        if device != "cuda":
-            print("no GPU available. Using CPU.") if verbose else None
-        else:
-            print(f"device: '{device}'") if verbose else None
-    else:
-        device = "cpu"
-        print(f"device: '{device}'") if verbose else None
-    return device
-
-
-def squeeze_integers(arr):
-    """The reference's gap-closing loop, as is (util.py:37-61): for each value in [0, max] missing
-    from the ORIGINAL array, every entry above it moves down by one while the loop runs, so
-    [0,2,2,5] -> [0,1,1,3] and [7,2,7,4,1] -> [5,1,5,3,0] (the reference's docstring claims
-    [3,2,3,1,0]; its code returns this)."""
-    uniques = np.unique(arr)
-    arr_squeezed = copy.deepcopy(arr)
-    for val in np.arange(0, np.max(arr) + 1):
-        if np.isin(val, uniques):
-            continue
-        arr_squeezed[arr_squeezed > val] = arr_squeezed[arr_squeezed > val] - 1
-    return arr_squeezed
-
-
-class WindowedDataset(Dataset):
-    """Windows of an untiled series (util.py:67-98): item idx = (X[idx+w0 : idx+w1], y[idx])."""
-
-    def __init__(self, X_untiled, y_input, win_range, transform=None, target_transform=None):
-        self.X_untiled = X_untiled
-        self.y_input = y_input
-        self.win_range = win_range
-        self.n_samples = y_input.shape[0]
-        self.usable_idx = torch.arange(-self.win_range[0], self.n_samples - self.win_range[1] + 1)
-        if X_untiled.shape[0] != y_input.shape[0]:
-            raise ValueError('RH: X and y must have same first dimension shape')
-
-    def __len__(self):
-        return self.n_samples
-
-    def check_bound_errors(self, idx):
-        idx_toRemove = []
-        for val in idx:
-            if (val + self.win_range[0] < 0) or (val + self.win_range[1] > self.n_samples):
-                idx_toRemove.append(val)
-        if len(idx_toRemove) > 0:
-            raise ValueError(f'RH: input idx is too close to edges. Remove idx: {idx_toRemove}')
-
-    def __getitem__(self, idx):
-        X_subset_tiled = self.X_untiled[idx + self.win_range[0]: idx + self.win_range[1]]
-        y_subset = self.y_input[idx]
-        return X_subset_tiled, y_subset
-
-
-def make_WindowedDataloader(X, y, win_range=[-10, 10], batch_size=64, drop_last=True, **kwargs_dataloader):
-    """Random-order minibatches of windows (util.py:100-114)."""
-    dataset = WindowedDataset(X, y, win_range)
-    sampler = torch.utils.data.SubsetRandomSampler(dataset.usable_idx, generator=None)
-    if kwargs_dataloader is None:
-        kwargs_dataloader = {'shuffle': False, 'pin_memory': False, 'num_workers': 0}
-    dataloader = DataLoader(dataset, batch_size=batch_size, drop_last=drop_last, sampler=sampler,
-                            **kwargs_dataloader)
-    dataloader.sample_shape = [dataloader.batch_size] + list(dataset[-win_range[0]][0].shape)
-    return dataloader, dataset, sampler
+def _usable_idx(T, win_range):
+    w0, w1 = int(win_range[0]), int(win_range[1])
+    return torch.arange(-w0, T - w1 + 1)
 
 
 def windowed_view(X_untiled, y, win_range):
-    """All windows of WindowedDataset(X_untiled, y, win_range) over `usable_idx`, in order, as a
-    zero-copy strided view: returns (Xw, yw) with Xw[n] == X_untiled[n : n + win_len] (the window
-    of idx = n - win_range[0]) and yw[n] == y[n - win_range[0]].
+    """All usable windows of the series, as (Xw, yw): Xw[n] == X_untiled[n : n + L] is the window
+    of idx = usable_idx[n] (idx + w0 == n), yw[n] == y[usable_idx[n]] (torch indexing, so a
+    positive w0 wraps to the end of y exactly as the reference's `y_input[idx]` does).
 
-    X_untiled must be contiguous (T, *F); Xw has shape (T - win_len + 1, win_len, *F) and
-    stride (F, F, *F-strides), i.e. consecutive samples overlap by win_len - 1 rows.
+    Xw is a zero-copy view of shape (T - L + 1, L, *F) and strides (F, F, *F-strides); only the
+    N targets are gathered.  X_untiled is made contiguous first if it is not.
     """
     X_untiled = torch.as_tensor(X_untiled)
     if not X_untiled.is_contiguous():
@@ -107,13 +44,42 @@ def windowed_view(X_untiled, y, win_range):
     n = T - L + 1
     if L < 1 or n < 1:
         raise ValueError(f"window {win_range} does not fit a series of length {T}")
-    feat = tuple(X_untiled.shape[1:])
-    F = int(np.prod(feat)) if feat else 1
-    inner = tuple(X_untiled.stride()[1:])
-    Xw = X_untiled.as_strided((n, L) + feat, (F, F) + inner)
     y = torch.as_tensor(y)
-    yw = y[-w0: -w0 + n]
+    if y.shape[0] != T:  # checked on the host: an out-of-range gather would fault on the device
+        raise ValueError(f"y must hold one target per series row: len(y) = {y.shape[0]}, series length {T}")
+    feat = tuple(X_untiled.shape[1:])
+    row = int(np.prod(feat)) if feat else 1
+    Xw = X_untiled.as_strided((n, L) + feat, (row, row) + tuple(X_untiled.stride()[1:]))
+    yw = y[_usable_idx(T, (w0, w1)).to(y.device)]
     return Xw, yw
+
+
+class WindowedDataset:
+    """Indexable windows of an untiled series with the reference's sample numbering (util.py:67-98).
+
+    `ds[idx]` for idx in `ds.usable_idx` returns (window, target) as views into the strided
+    `ds.windows` / gathered `ds.targets` (the tensors a fit takes directly).  Deviation: an idx
+    outside `usable_idx` raises IndexError, where the reference returns a truncated window.
+    `len(ds)` is the number of usable windows (the reference reports the series length).
+    """
+
+    def __init__(self, X_untiled, y_input, win_range):
+        if len(X_untiled) != len(y_input):
+            raise ValueError(f"X_untiled and y_input need the same length along dim 0, got "
+                             f"{len(X_untiled)} and {len(y_input)}")
+        self.win_range = (int(win_range[0]), int(win_range[1]))
+        self.windows, self.targets = windowed_view(X_untiled, y_input, self.win_range)
+        self.usable_idx = _usable_idx(len(X_untiled), self.win_range)
+
+    def __len__(self):
+        return int(self.windows.shape[0])
+
+    def __getitem__(self, idx):
+        n = int(idx) + self.win_range[0]
+        if not 0 <= n < len(self):
+            raise IndexError(f"window index {int(idx)} is outside usable_idx "
+                             f"[{int(self.usable_idx[0])}, {int(self.usable_idx[-1])}]")
+        return self.windows[n], self.targets[n]
 
 
 class HostStream:

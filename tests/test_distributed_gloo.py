@@ -5,8 +5,9 @@ the plan's data-gradient entry point, all-reduces the packed gradient arena, the
 Adam step. Here the HIP plan is replaced by `OraclePlan`, a test double with the same interface
 that computes shard gradients with the oracle. The real loop then runs sample-sharded over gloo
 and is compared with the unsharded run. This covers the sharding, the global normalisation, the
-all-reduce placement, the device-side history and stop-flag bookkeeping, and the replica
-lock-step, all without a GPU.
+all-reduce placement, the device-side history and stop-flag bookkeeping, the replica
+lock-step, the start-of-fit replica synchronisation (ranks initialised differently) and the
+recovery from a pass that failed on the device on one rank only, all without a GPU.
 """
 import os
 import socket
@@ -18,24 +19,32 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from oracle import cp_oracle
+from tensor_regression_amd import _lib
 from tensor_regression_amd._engine import adam_hparams, run_adam_fit
 
 
 class OraclePlan:
     """Same interface as _engine.Plan, computed on the CPU with the oracle (tests only)."""
 
-    def __init__(self, model, shapes, non_negative, has_bias):
+    def __init__(self, model, shapes, non_negative, has_bias, fail_at=None):
         self.model = model
+        self.fail_at = fail_at  # (simulated) device failure of the local pass at this Adam step
+        self.step_seen = 0
+        self.recovered = []
         self.shapes = shapes
         self.non_negative = non_negative
         self.has_bias = has_bias
         self.offsets = np.cumsum([0] + [a * b for a, b in shapes]).tolist()
         self.num_params = self.offsets[-1] + (1 if has_bias else 0)
-        self.num_grads = self.num_params + 1
+        self.num_grads = self.num_params + 2  # + data loss + device status
         self.device_str = "cpu"
 
     def check_status(self):
         pass
+
+    def recover(self, where):
+        self.recovered.append(where)
+        self.fail_at = None
 
     def factors(self, arena):
         return [arena[self.offsets[f]:self.offsets[f + 1]].view(s).clone() for f, s in enumerate(self.shapes)]
@@ -58,10 +67,18 @@ class OraclePlan:
             data = torch.sum(-cw * logq[torch.arange(X.shape[0]), target]) / norm
             data.backward()
             grad[:self.offsets[-1]] = torch.cat([a.grad.reshape(-1) for a in Bcp])
-        grad[-1] = data.detach()
+        grad[self.num_params] = data.detach()
+        self.step_seen += 1
+        failed = self.fail_at is not None and self.step_seen == self.fail_at
+        if failed:  # what k_linear_cluster leaves behind: NaN partials + the status slot
+            grad[:self.num_params + 1] = float("nan")
+        grad[self.num_params + 1] = 1.0 if failed else 0.0
 
     def adam_step(self, arena, grad, m, v, vmax, lam, hp, step, hist, base, it, patience, tol, stop):
         if int(stop.item()):
+            return
+        if float(grad[self.num_params + 1]) != 0.0:  # k_update: failed pass -> stop, apply nothing
+            stop[0] = _lib.TR_STOP_DEVICE_ERROR - it
             return
         nfe = self.offsets[-1]
         norms = [torch.sqrt(torch.sum(arena[self.offsets[f]:self.offsets[f + 1]] ** 2))
@@ -82,7 +99,7 @@ class OraclePlan:
             den_src = vmax
         denom = den_src.sqrt() / (bc2 ** 0.5) + hp["eps"]
         arena[:self.num_params].addcdiv_(m, denom, value=-hp["lr"] / bc1)
-        total = float(grad[-1]) + lam * float(sum(norms))
+        total = float(grad[self.num_params]) + lam * float(sum(norms))
         hist[base + it] = total
         if it > patience and tol > 0:
             h = hist[it - patience: base + it + 1].numpy()
@@ -110,26 +127,49 @@ def _problem(model):
     return X, y, cw, norm, shapes, arena0
 
 
-def _fit(model, X, y, cw, norm, shapes, arena0, allreduce=None, iters=25, tol=0.0, patience=5):
-    plan = OraclePlan(model, shapes, [False] * len(shapes), model == "linear")
+def _fit(model, X, y, cw, norm, shapes, arena0, process_group=None, iters=25, tol=0.0, patience=5, fail_at=None):
+    plan = OraclePlan(model, shapes, [False] * len(shapes), model == "linear", fail_at=fail_at)
     arena = arena0.clone()
     loss_running = []
     hp = adam_hparams({"lr": 0.02, "amsgrad": model != "linear"})
     conv, n = run_adam_fit(plan, X, y, cw, norm, arena, torch.ones(shapes[0][1]), 0.01, iters, tol, patience, hp,
-                           loss_running, allreduce=allreduce, sync_every=7)
-    return arena, loss_running, conv
+                           loss_running, process_group=process_group, sync_every=7)
+    return arena, loss_running, conv, plan
 
 
-def _worker(rank, world, port, model, tol, out_path):
+def _worker(rank, world, port, model, tol, out_path, variant="plain"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.set_num_threads(1)
     X, y, cw, norm, shapes, arena0 = _problem(model)
+    if variant == "seeds" and rank == 1:  # a replica initialised differently: sync_replicas takes rank 0's
+        arena0 = torch.randn(arena0.shape, generator=torch.Generator().manual_seed(123))
+    fail_at = 10 if (variant == "fail" and rank == 1) else None  # rank 1's 10th pass fails on the "device"
     lo, hi = [(0, 40), (40, 96)][rank]  # uneven shards
-    arena, lr_, conv = _fit(model, X[lo:hi].contiguous(), y[lo:hi].contiguous(), cw, norm, shapes, arena0,
-                            allreduce=lambda g: dist.all_reduce(g), tol=tol)
-    torch.save({"arena": arena, "loss_running": lr_, "conv": conv}, f"{out_path}.{rank}")
+    arena, lr_, conv, plan = _fit(model, X[lo:hi].contiguous(), y[lo:hi].contiguous(), cw, norm, shapes, arena0,
+                                  process_group=dist.group.WORLD, tol=tol, fail_at=fail_at)
+    torch.save({"arena": arena, "loss_running": lr_, "conv": conv, "recovered": plan.recovered}, f"{out_path}.{rank}")
+    dist.destroy_process_group()
+
+
+def _worker_mismatch(rank, world, port, out_path):
+    """Rank 1's model has a different arena size (a multinomial shard missing a class): every rank
+    must raise instead of hanging in the per-iteration all-reduce."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    X, y, cw, norm, shapes, arena0 = _problem("multinomial")
+    if rank == 1:
+        shapes = shapes[:-1] + [(shapes[-1][0] - 1, shapes[-1][1])]
+        arena0 = arena0[:sum(a * b for a, b in shapes)]
+    try:
+        _fit("multinomial", X, y, cw, norm, shapes, arena0, process_group=dist.group.WORLD, iters=3)
+        res = "no error"
+    except ValueError as e:
+        res = "ValueError" if "disagree" in str(e) else f"other: {e}"
+    with open(f"{out_path}.{rank}", "w") as f:
+        f.write(res)
     dist.destroy_process_group()
 
 
@@ -145,7 +185,7 @@ def _free_port():
 def test_sharded_fit_matches_unsharded(tmp_path, model, tol):
     torch.set_num_threads(1)
     X, y, cw, norm, shapes, arena0 = _problem(model)
-    ref_arena, ref_loss, ref_conv = _fit(model, X, y, cw, norm, shapes, arena0, tol=tol)
+    ref_arena, ref_loss, ref_conv, _ = _fit(model, X, y, cw, norm, shapes, arena0, tol=tol)
     out = str(tmp_path / "res")
     mp.spawn(_worker, args=(2, _free_port(), model, tol, out), nprocs=2, join=True)
     r0 = torch.load(out + ".0", weights_only=True)
@@ -159,3 +199,38 @@ def test_sharded_fit_matches_unsharded(tmp_path, model, tol):
     np.testing.assert_allclose(r0["loss_running"], ref_loss, rtol=2e-5)
     rel = float(torch.linalg.norm(r0["arena"] - ref_arena) / torch.linalg.norm(ref_arena))
     assert rel < 1e-4, rel
+
+
+@pytest.mark.parametrize("variant", ["seeds", "fail"])
+def test_sharded_fit_sync_and_device_failure(tmp_path, variant):
+    """seeds: rank 1 starts from other parameters -> both ranks still reproduce the unsharded fit
+    from rank 0's init (one broadcast at fit start).  fail: rank 1's local pass fails on the
+    device at step 10 -> the all-reduced status slot stops BOTH ranks before that step, both
+    recover at the same iteration, and the fit ends exactly where the failure-free fit ends."""
+    torch.set_num_threads(1)
+    model = "linear"
+    X, y, cw, norm, shapes, arena0 = _problem(model)
+    ref_arena, ref_loss, _, _ = _fit(model, X, y, cw, norm, shapes, arena0)
+    out = str(tmp_path / "res")
+    mp.spawn(_worker, args=(2, _free_port(), model, 0.0, out, variant), nprocs=2, join=True)
+    r0 = torch.load(out + ".0", weights_only=True)
+    r1 = torch.load(out + ".1", weights_only=True)
+    assert torch.equal(r0["arena"], r1["arena"])
+    assert r0["loss_running"] == r1["loss_running"]
+    assert len(r0["loss_running"]) == len(ref_loss)
+    np.testing.assert_allclose(r0["loss_running"], ref_loss, rtol=2e-5)
+    rel = float(torch.linalg.norm(r0["arena"] - ref_arena) / torch.linalg.norm(ref_arena))
+    assert rel < 1e-4, rel
+    if variant == "fail":
+        assert r0["recovered"] == r1["recovered"] == ["iteration 9"]
+        assert all(np.isfinite(r0["loss_running"]))
+    else:
+        assert r0["recovered"] == r1["recovered"] == []
+
+
+def test_rank_mismatch_raises_everywhere(tmp_path):
+    out = str(tmp_path / "mm")
+    mp.spawn(_worker_mismatch, args=(2, _free_port(), out), nprocs=2, join=True)
+    for r in range(2):
+        with open(f"{out}.{r}") as f:
+            assert f.read() == "ValueError"

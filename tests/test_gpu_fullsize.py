@@ -88,7 +88,7 @@ def _linear_case(shape, rank, seed):
     plan.loss_grad(X, y, None, float(shape[0]), arena, model.weights, grad)
     plan.finalize_grad(arena, grad, lam, gtot, loss)
     data, total, grads, dbias = _linear_fp64(X, y, model.Bcp, model.bias.item(), lam)
-    errs = {"data_loss": abs(grad[-1].item() - data) / abs(data), "loss": abs(loss.item() - total) / abs(total),
+    errs = {"data_loss": abs(grad[plan.num_params].item() - data) / abs(data), "loss": abs(loss.item() - total) / abs(total),
             "bias": abs(gtot[plan.offsets[-1]].item() - dbias) / max(abs(dbias), 1e-30)}
     for f, (v, ref) in enumerate(zip(plan.factor_views(gtot), grads)):
         errs[f"grad{f}"] = normwise_rel(v.cpu().numpy(), ref.cpu().numpy())
@@ -157,7 +157,7 @@ def test_multinomial_full_size_vs_fp64():
     pen, pg = _l2(A64, lam)
     data = float(nll) / wsum
     total = data + float(pen)
-    errs = {"data_loss": abs(grad[-1].item() - data) / abs(data), "loss": abs(loss.item() - total) / abs(total)}
+    errs = {"data_loss": abs(grad[plan.num_params].item() - data) / abs(data), "loss": abs(loss.item() - total) / abs(total)}
     for f, (v, ref, q) in enumerate(zip(plan.factor_views(gtot), grads, pg)):
         errs[f"grad{f}"] = normwise_rel(v.cpu().numpy(), (ref + q).cpu().numpy())
     print("c3", plan.describe, errs)

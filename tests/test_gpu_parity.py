@@ -202,7 +202,7 @@ def test_linear_lbfgs_golden():
     model.fit(X, y, lambda_L2=m["lambda_L2"], max_iter=m["max_iter"], tol=0.0, patience=100,
               running_loss_logging_interval=m["logging_interval"], LBFGS_kwargs=m["lbfgs_kwargs"])
     assert len(model.loss_running) == len(d["loss_running"])
-    np.testing.assert_allclose(model.loss_running, d["loss_running"], rtol=1e-4)
+    np.testing.assert_allclose(model.loss_running, d["loss_running"], rtol=RTOL)
     # strong-Wolfe LBFGS on a scale-ambiguous CP objective: compare the identifiable dense
     # coefficient tensor B, as accurately as the reference's own fp32 run tracks the fp64 one
     from oracle import cp_oracle
@@ -212,6 +212,67 @@ def test_linear_lbfgs_golden():
     dense = lambda F: cp_oracle.dense_from_factors_np([np.asarray(f, np.float64) for f in F], np.ones(m["rank"]))
     ours = dense([a.detach().cpu().numpy() for a in model.Bcp])
     _assert_as_accurate_as_reference([ours], [dense(d["Bcp_final_list"])], [dense(r64["Bcp"])], tol=1e-4)
+
+
+@pytest.mark.parametrize("name", names("mnllbfgs_"))
+def test_multinomial_lbfgs_golden(name):
+    """CP_logistic_regression.fit (LBFGS, multinomial…py:291-387): torch.optim.LBFGS drives the
+    factors, every closure's loss + gradient comes from the HIP kernels.
+
+    Multinomial LBFGS is ill-conditioned in fp32: the reference's own fp32 run differs from the
+    fp64 restatement of the same algorithm by 3.7e-2 at the first logged step of mnllbfgs_basic
+    (strong-Wolfe, 20 inner iterations) and by 4e-4 after 6 steps of mnllbfgs_weighted (no line
+    search, 3 inner iterations), and the double-softmax loss is so flat that the reference's fp32
+    and fp64 runs end 11 % apart in the dense coefficient tensor.  So: the closure itself is held
+    to the one-step bar (loss 1e-6, gradients 1e-5 vs the oracle) at the initial point, and at the
+    point the GPU fit ends — near a stationary point, where the gradient is small against its fp32
+    summation noise — to within 2x the oracle's own fp32 error against the fp64 closed form; the
+    first logged loss to 1e-5; every later logged loss within 1e-5 of
+    the reference's fp32 run OR no further from the fp64 run than the reference's fp32 run is
+    (x2).  Parameters are not compared: they are not identified by this trajectory."""
+    from tensor_regression_amd import CP_logistic_regression
+    from oracle import cp_oracle
+    d = load(name)
+    m = d["meta"]
+    Bcp = [torch.tensor(a, device=DEV).requires_grad_(True) for a in d["Bcp0_list"]]
+    mm = CP_logistic_regression(d["X"].numpy(), d["y"], rank=m["rank"], Bcp_init=Bcp, device=DEV)
+    def closure_parity(final=False):
+        dev, Xd, yd = mm._device_data()
+        plan = mm._get_plan(Xd, Xd.shape[0])
+        cw, W = mm._class_weights(np.array(m["class_weights"]), dev, yd)
+        arena = plan.pack(mm.Bcp)
+        grad = torch.zeros(plan.num_grads, device=DEV)
+        gtot = torch.zeros(plan.num_params, device=DEV)
+        loss = torch.zeros(1, device=DEV)
+        plan.loss_grad(Xd, yd, cw, W, arena, mm.weights.to(DEV), grad)
+        plan.finalize_grad(arena, grad, m["lambda_L2"], gtot, loss)
+        r0 = cp_oracle.mnl_loss_grad(d["X"], d["y"], [a.detach().cpu().numpy() for a in mm.Bcp], np.ones(m["rank"]),
+                                     m["non_negative"], m["class_weights"], m["lambda_L2"])
+        assert abs(loss.item() - r0["loss"]) <= 1e-6 * abs(r0["loss"])
+        if not final:
+            _assert_factors(plan.factor_views(gtot), r0["grads"])
+            return
+        c64 = cp_oracle.closed_form_mnl(d["X"].double().numpy(), d["y"], [a.detach().cpu().numpy() for a in mm.Bcp],
+                                        np.ones(m["rank"]), m["non_negative"], m["class_weights"], m["lambda_L2"])
+        for g, o, w in zip(plan.factor_views(gtot), r0["grads"], c64["grads"]):
+            e_ours = np.linalg.norm(g.cpu().numpy().astype(np.float64) - w)
+            e_ora = np.linalg.norm(np.asarray(o, np.float64) - w)
+            assert e_ours <= 2 * e_ora + RTOL * np.linalg.norm(w), (e_ours, e_ora, np.linalg.norm(w))
+
+    closure_parity()
+    conv = mm.fit(lambda_L2=m["lambda_L2"], max_iter=m["max_iter"], tol=0.0, patience=100,
+                  weights=np.array(m["class_weights"]), running_loss_logging_interval=m["logging_interval"],
+                  LBFGS_kwargs=m["lbfgs_kwargs"])
+    assert int(conv) == int(d["converged"])
+    assert len(mm.loss_running) == len(d["loss_running"])
+    r64 = cp_oracle.fit_lbfgs_mnl(d["X"], d["y"], d["Bcp0_list"], np.ones(m["rank"]), m["non_negative"],
+                                  m["class_weights"], m["lambda_L2"], m["max_iter"], 0.0, 100, m["logging_interval"],
+                                  m["lbfgs_kwargs"], dtype=torch.float64)
+    ours, ref32, ref64 = (np.asarray(v, np.float64) for v in (mm.loss_running, d["loss_running"], r64["loss_running"]))
+    assert abs(ours[0] - ref32[0]) <= RTOL * abs(ref32[0])
+    ok = (np.abs(ours - ref32) <= RTOL * np.abs(ref32)) | (np.abs(ours - ref64) <= 2 * np.abs(ref32 - ref64) + RTOL * np.abs(ref64))
+    assert ok.all(), (ours, ref32, ref64)
+    closure_parity(final=True)  # the kernels at the point the GPU trajectory reached
 
 
 # ------------------------------------------------------------------------------------------------
@@ -259,7 +320,7 @@ def test_linear_sweep_vs_oracle(shape, rank, kind):
         loss = torch.zeros(1, device=DEV)
         plan.loss_grad(Xd, yd, None, float(shape[0]), arena, model.weights, grad)
         plan.finalize_grad(arena, grad, lam, gtot, loss)
-        assert abs(grad[-1].item() - ref["data_loss"]) <= RTOL * abs(ref["data_loss"])
+        assert abs(grad[plan.num_params].item() - ref["data_loss"]) <= RTOL * abs(ref["data_loss"])
         assert abs(loss.item() - ref["loss"]) <= RTOL * abs(ref["loss"])
         _assert_factors(plan.factor_views(gtot), ref["grads"])
         yh = plan.forward(Xd, arena, model.weights)
@@ -539,3 +600,37 @@ def test_prepare_next_bitwise_equals_separate_prep(case):
         assert outs[0][0] and len(outs[0][1]) == 6
     for a, b in zip(outs[0][2], outs[1][2]):
         assert np.array_equal(a, b)
+
+
+# ------------------------------------------------------------------------------------------------
+# wide-row cluster pass failing on the device (GPU shared): the fit stops before applying the
+# failed step on the all-reduced status slot and resumes on the two-pass path
+# ------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("policy", ["fallback", "raise"])
+def test_cluster_device_failure(monkeypatch, policy):
+    from tensor_regression_amd import CP_linear_regression, _engine
+    g = torch.Generator().manual_seed(5)
+    X = torch.randn(300, 64, 64, 32, generator=g).to(DEV)
+    y = torch.randn(300, generator=g).to(DEV)
+
+    def fit(iters):
+        torch.manual_seed(3)
+        m = CP_linear_regression(X.shape, rank=4, device=DEV)
+        m.fit_Adam(X, y, lambda_L2=0.01, max_iter=iters, tol=0, patience=10, Adam_kwargs={"lr": 0.01})
+        return m
+
+    with path("twopass"):
+        ref = fit(12)
+    monkeypatch.setenv("TR_CLUSTER_SPIN_LIMIT", "0")  # every exchange of the cluster pass times out
+    monkeypatch.setattr(_engine, "_ON_DEVICE_ERROR", policy)
+    with path("auto"):
+        if policy == "raise":
+            with pytest.raises(RuntimeError, match="failed on the device"):
+                fit(12)
+            return
+        with pytest.warns(RuntimeWarning, match="two-pass"):
+            m = fit(12)
+    assert "cluster-1pass" in m._plan.describe and "recovered=2pass" in m._plan.describe
+    assert len(m.loss_running) == 12 and np.all(np.isfinite(m.loss_running))
+    np.testing.assert_allclose(m.loss_running, ref.loss_running, rtol=RTOL)
+    _assert_factors(m.Bcp, [a.detach().cpu().numpy() for a in ref.Bcp])

@@ -1,43 +1,81 @@
-"""util.py parity (WindowedDataset / make_WindowedDataloader / squeeze_integers, reference
-util.py:15-114) and the zero-copy windowed view on the CPU; the windowed and host-streamed fits on
-the GPU (gpu-marked)."""
+"""Windowed / out-of-core data path (reference util.py:67-98 WindowedDataset).
+
+CPU: windowed_view / WindowedDataset reproduce the reference's windows, pinned by the win_*
+fixtures (tools/gen_golden.py stacks the reference WindowedDataset's samples and fits them with
+the reference's own fit_Adam): the oracle fitted on our windows reproduces those fixtures bit for
+bit.  GPU (gpu-marked): fit_Adam over the strided windowed view, over the materialised windows and
+over a HostStream of them, each against the same fixtures at the 1e-5 parity bar; plus
+windowed-vs-materialised bitwise checks on wider shapes."""
 import numpy as np
 import pytest
 import torch
 
+from golden_util import load, names, normwise_rel
 from tensor_regression_amd import util
 
-
-def test_squeeze_integers():
-    # the reference's own output for its docstring example (util.py:37-61; the docstring's
-    # "[3,2,3,1,0]" is not what its code returns)
-    np.testing.assert_array_equal(util.squeeze_integers(np.array([7, 2, 7, 4, 1])), [5, 1, 5, 3, 0])
-    # (values are shifted while the loop runs, so gaps above a shifted value can stay)
-    np.testing.assert_array_equal(util.squeeze_integers(np.array([0, 2, 2, 5])), [0, 1, 1, 3])
-    np.testing.assert_array_equal(util.squeeze_integers(np.array([3, 3, 1])), [2, 2, 0])
+WIN = names("win_")
 
 
-@pytest.mark.parametrize("win_range", [(-3, 4), (0, 5), (-6, 1)])
-def test_windowed_view_matches_dataset(win_range):
+def _windows(d):
+    """The fixture's series -> (windows view, targets) through our windowed_view."""
+    m = d["meta"]
+    S = d["X"]  # the untiled series (X_q / 8)
+    y = torch.tensor(d["y_series"])
+    return util.windowed_view(S, y, m["win_range"])
+
+
+@pytest.mark.parametrize("win_range", [(-3, 4), (0, 5), (-6, 1), (2, 6)])
+def test_windowed_dataset_indexing(win_range):
+    """WindowedDataset numbering: ds[idx] == X[idx + w0 : idx + w1], y[idx] for idx in usable_idx
+    (reference util.py:72, 93-96), zero-copy over the series."""
     g = torch.Generator().manual_seed(0)
     X = torch.randn(40, 5, 3, generator=g)
     y = torch.randn(40, generator=g)
     ds = util.WindowedDataset(X, y, list(win_range))
-    Xw, yw = util.windowed_view(X, y, win_range)
-    assert Xw.shape == (len(ds.usable_idx), win_range[1] - win_range[0], 5, 3)
-    assert Xw.stride(0) == 15 and Xw.data_ptr() == X.data_ptr()  # no copy
-    for n, idx in enumerate(ds.usable_idx.tolist()):
+    w0, w1 = win_range
+    assert torch.equal(ds.usable_idx, torch.arange(-w0, 40 - w1 + 1))
+    assert ds.windows.shape == (len(ds.usable_idx), w1 - w0, 5, 3)
+    assert ds.windows.stride(0) == 15 and ds.windows.data_ptr() == X.data_ptr()  # no copy
+    for idx in ds.usable_idx.tolist():
         xi, yi = ds[idx]
-        assert torch.equal(Xw[n], xi) and torch.equal(yw[n], yi)
+        assert torch.equal(xi, X[idx + w0: idx + w1]) and torch.equal(yi, y[idx])
+    with pytest.raises(IndexError):
+        ds[int(ds.usable_idx[-1]) + 1]
+    with pytest.raises(ValueError):
+        util.WindowedDataset(X, y[:-1], list(win_range))
+    with pytest.raises(ValueError):  # a target vector of the wrong length is refused on the host
+        util.windowed_view(X, y[:-2], win_range)
 
 
-def test_windowed_dataloader_shapes():
-    X = torch.randn(100, 8)
-    y = torch.randn(100)
-    dl, ds, _ = util.make_WindowedDataloader(X, y, win_range=[-5, 5], batch_size=16)
-    xb, yb = next(iter(dl))
-    assert tuple(xb.shape) == (16, 10, 8) and tuple(yb.shape) == (16,)
-    assert dl.sample_shape == [16, 10, 8]
+@pytest.fixture()
+def _one_thread():
+    n = torch.get_num_threads()
+    torch.set_num_threads(1)  # fixtures were produced single-threaded (fixed summation order)
+    yield
+    torch.set_num_threads(n)
+
+
+@pytest.mark.parametrize("name", WIN)
+def test_oracle_on_windowed_view_matches_reference(name, _one_thread):
+    """The reference's WindowedDataset samples, fitted by the reference fit_Adam (fixture), are
+    reproduced bit for bit by the oracle run on OUR windows: pins windowed_view to util.py:67-98."""
+    from oracle import cp_oracle
+    d = load(name)
+    m = d["meta"]
+    Xw, yw = _windows(d)
+    assert Xw.shape[0] == m["n_windows"] and list(Xw.shape[1:]) == m["window_shape"]
+    ones = np.ones(m["rank"], np.float32)
+    X = Xw.contiguous()
+    if m["n_classes"]:
+        f = cp_oracle.fit_adam_mnl(X, yw, d["Bcp0_list"], ones, m["non_negative"], np.ones(m["n_classes"]),
+                                   m["lambda_L2"], m["max_iter"], m["tol"], m["patience"], m["adam_kwargs"],
+                                   m["softplus_kwargs"])
+    else:
+        f = cp_oracle.fit_adam_linear(X, yw, d["Bcp0_list"], d["bias0"], ones, m["non_negative"], m["lambda_L2"],
+                                      m["max_iter"], m["tol"], m["patience"], m["adam_kwargs"], m["softplus_kwargs"])
+    np.testing.assert_array_equal(np.array(f["loss_running"]), d["loss_running"])
+    for a, b in zip(f["Bcp"], d["Bcp_final_list"]):
+        np.testing.assert_array_equal(a, b)
 
 
 def test_rows_contiguous_detection():
@@ -136,3 +174,85 @@ def test_host_stream_fit_matches_resident():
         m.fit_Adam(XX, ys.to(DEV), lambda_L2=0.01, max_iter=10, tol=0, patience=10, Adam_kwargs={"lr": 0.01})
         res.append(np.array(m.loss_running))
     np.testing.assert_allclose(res[1], res[0], rtol=1e-5)
+
+
+def _assert_close_factors(got, want, tol=1e-5):
+    for a, b in zip(got, want):
+        a = a.detach().cpu().numpy() if isinstance(a, torch.Tensor) else a
+        assert normwise_rel(a, b) <= tol, (normwise_rel(a, b), a.shape)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("source", ["view", "materialised", "hoststream"])
+@pytest.mark.parametrize("name", [n for n in WIN if not n.startswith("win_mnl")])
+def test_windowed_linear_golden(name, source):
+    """fit_Adam over the windowed data vs the reference's fit of its WindowedDataset samples:
+    one loss + gradient at the init point, the 10-iteration factors and the full loss trajectory
+    at 1e-5 (SURVEY §8(c) parity definition)."""
+    from tensor_regression_amd import CP_linear_regression
+    d = load(name)
+    m = d["meta"]
+    Xw, yw = _windows(d)
+    yd = yw.to(DEV)
+    if source == "view":
+        XX = util.windowed_view(d["X"].to(DEV), torch.tensor(d["y_series"], device=DEV), m["win_range"])[0]
+        assert XX.stride(0) != int(np.prod(XX.shape[1:]))  # really the overlapping view
+    elif source == "materialised":
+        XX = Xw.contiguous().to(DEV)
+    else:
+        XX = util.HostStream(Xw.contiguous(), chunk_rows=max(1, Xw.shape[0] // 3), device=DEV)
+
+    def make():
+        Bcp = [torch.tensor(a, device=DEV).requires_grad_(True) for a in d["Bcp0_list"]]
+        return CP_linear_regression((Xw.shape[0],) + tuple(Xw.shape[1:]), rank=m["rank"], Bcp_init=Bcp,
+                                    bias_init=float(d["bias0"][0]), device=DEV)
+
+    if source != "hoststream":
+        model = make()
+        plan = model._get_plan(XX, XX.shape[0])
+        arena = plan.pack(model.Bcp, model.bias)
+        grad = torch.zeros(plan.num_grads, device=DEV)
+        gtot = torch.zeros(plan.num_params, device=DEV)
+        loss = torch.zeros(1, device=DEV)
+        plan.loss_grad(XX, yd, None, float(XX.shape[0]), arena, model.weights, grad)
+        plan.finalize_grad(arena, grad, m["lambda_L2"], gtot, loss)
+        assert abs(loss.item() - d["loss0"]) <= 1e-5 * abs(d["loss0"])
+        _assert_close_factors(plan.factor_views(gtot), d["grads0_list"])
+    m10 = make()
+    m10.fit_Adam(XX, yd, lambda_L2=m["lambda_L2"], max_iter=10, tol=0, patience=10, Adam_kwargs=m["adam_kwargs"])
+    np.testing.assert_allclose(m10.loss_running, d["loss_running_10"], rtol=1e-5)
+    _assert_close_factors(m10.Bcp, d["Bcp_10_list"])
+    model = make()
+    model.fit_Adam(XX, yd, lambda_L2=m["lambda_L2"], max_iter=m["max_iter"], tol=0, patience=10,
+                   Adam_kwargs=m["adam_kwargs"])
+    assert len(model.loss_running) == len(d["loss_running"])
+    np.testing.assert_allclose(model.loss_running, d["loss_running"], rtol=1e-5)
+    _assert_close_factors(model.Bcp, d["Bcp_final_list"], tol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("source", ["view", "materialised"])
+def test_windowed_multinomial_golden(source):
+    from tensor_regression_amd import CP_logistic_regression
+    d = load("win_mnl")
+    m = d["meta"]
+    Xw, yw = _windows(d)
+    XX = (util.windowed_view(d["X"].to(DEV), torch.tensor(d["y_series"], device=DEV), m["win_range"])[0]
+          if source == "view" else Xw.contiguous().to(DEV))
+
+    def make():
+        return CP_logistic_regression(XX, yw.numpy(), rank=m["rank"], device=DEV,
+                                      Bcp_init=[torch.tensor(a, device=DEV) for a in d["Bcp0_list"]])
+
+    from tensor_regression_amd.multinomial_tensor_regression import model as mnl_model
+    mm = make()
+    S = mnl_model(XX, mm.Bcp, mm.weights, mm.non_negative, mm.softplus_kwargs)
+    np.testing.assert_allclose(S.cpu().numpy(), d["probs0"], rtol=1e-5, atol=1e-6)
+    m10 = make()
+    m10.fit_Adam(lambda_L2=m["lambda_L2"], max_iter=10, tol=0, patience=10, weights=np.ones(m["n_classes"]),
+                 Adam_kwargs=m["adam_kwargs"])
+    np.testing.assert_allclose(m10.loss_running, d["loss_running_10"], rtol=1e-5)
+    _assert_close_factors(m10.Bcp, d["Bcp_10_list"])
+    mm.fit_Adam(lambda_L2=m["lambda_L2"], max_iter=m["max_iter"], tol=0, patience=10,
+                weights=np.ones(m["n_classes"]), Adam_kwargs=m["adam_kwargs"])
+    np.testing.assert_allclose(mm.loss_running, d["loss_running"], rtol=1e-5)

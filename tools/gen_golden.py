@@ -30,6 +30,7 @@ sys.dont_write_bytecode = True
 import standard_tensor_regression as STR  # noqa: E402  (reference)
 import multinomial_tensor_regression as MTR  # noqa: E402  (reference)
 import spectral_tensor_regression as SPR  # noqa: E402  (reference)
+import util as RUTIL  # noqa: E402  (reference util.py: WindowedDataset)
 
 OUT = os.path.join(REPO, "tests", "golden")
 
@@ -45,11 +46,26 @@ def save(name, **arrays):
     print("wrote", path, os.path.getsize(path), "bytes")
 
 
+def planted_y(rng, Xq, rank):
+    """configs[0] recipe: y = <X, [[A*]]> + 0.1 N(0,1) with A* ~ N(0,1) of rank `rank`,
+    evaluated in fp64 from the exact int8/8 X, stored as fp32."""
+    A = [rng.standard_normal((d, rank)) for d in Xq.shape[1:]]
+    B = A[0]
+    for a in A[1:]:
+        B = (B[:, None, :] * a[None, :, :]).reshape(-1, rank)
+    Bd = B.sum(1)
+    Xf = Xq.reshape(Xq.shape[0], -1).astype(np.float64) / 8.0
+    return torch.tensor((Xf @ Bd + 0.1 * rng.standard_normal(Xq.shape[0])).astype(np.float32))
+
+
 def linear_case(name, seed, shape, rank, non_negative, bias_init, lam, adam_kwargs, iters, tol=0.0, patience=10,
-                softplus=None, second_fit=0):
+                softplus=None, second_fit=0, planted=False):
     rng = np.random.default_rng(seed)
     Xq, X = exact_X(rng, shape)
-    y = torch.tensor(rng.standard_normal(shape[0]).astype(np.float32))
+    if planted:
+        y = planted_y(rng, Xq, rank)
+    else:
+        y = torch.tensor(rng.standard_normal(shape[0]).astype(np.float32))
     torch.manual_seed(seed)
     m = STR.CP_linear_regression(X.shape, rank=rank, non_negative=non_negative, bias_init=bias_init,
                                  softplus_kwargs=softplus)
@@ -89,7 +105,7 @@ def linear_case(name, seed, shape, rank, non_negative, bias_init, lam, adam_kwar
                    bias_final2=m.bias.detach().numpy().copy())
     meta = dict(model="linear", seed=seed, shape=list(shape), rank=rank, non_negative=list(map(bool, non_negative)),
                 bias_init=bias_init, lambda_L2=lam, adam_kwargs=adam_kwargs, max_iter=iters, tol=tol,
-                patience=patience, softplus_kwargs=m.softplus_kwargs, second_fit=second_fit,
+                patience=patience, softplus_kwargs=m.softplus_kwargs, second_fit=second_fit, planted=planted,
                 factor_shapes=[list(a.shape) for a in Bcp0], torch=torch.__version__)
     out["meta"] = np.array(json.dumps(meta))
     save(name, **out)
@@ -147,6 +163,102 @@ def mnl_case(name, seed, shape, n_classes, rank, non_negative, class_w, lam, ada
          Bcp_final=np.concatenate([A.detach().numpy().reshape(-1) for A in m.Bcp]), converged=np.int32(conv),
          Bcp_10=np.concatenate([A.detach().numpy().reshape(-1) for A in m10.Bcp]),
          loss_running_10=np.array(m10.loss_running), meta=np.array(json.dumps(meta)))
+
+
+def mnl_lbfgs_case(name, seed, shape, n_classes, rank, class_w, lam, iters, lbfgs_kwargs, logging_interval=1):
+    """CP_logistic_regression.fit (LBFGS, multinomial…py:291-387): logged loss = data CE only (:372)."""
+    rng = np.random.default_rng(seed)
+    Xq, X = exact_X(rng, shape)
+    y = rng.integers(0, n_classes, size=shape[0])
+    y[:n_classes] = np.arange(n_classes)
+    torch.manual_seed(seed)
+    m = MTR.CP_logistic_regression(X.numpy(), y, rank=rank)
+    Bcp0 = [A.detach().numpy().copy() for A in m.Bcp]
+    conv = m.fit(lambda_L2=lam, max_iter=iters, tol=0.0, patience=100, weights=np.asarray(class_w), verbose=False,
+                 running_loss_logging_interval=logging_interval, LBFGS_kwargs=dict(lbfgs_kwargs))
+    meta = dict(model="multinomial_lbfgs", seed=seed, shape=list(shape), n_classes=n_classes, rank=rank,
+                class_weights=list(map(float, class_w)), lambda_L2=lam, max_iter=iters, lbfgs_kwargs=lbfgs_kwargs,
+                logging_interval=logging_interval, non_negative=[False] * (len(shape)),
+                softplus_kwargs=m.softplus_kwargs, factor_shapes=[list(a.shape) for a in Bcp0],
+                torch=torch.__version__)
+    save(name, X_q=Xq, y=y.astype(np.int64), Bcp0=np.concatenate([a.reshape(-1) for a in Bcp0]),
+         loss_running=np.array(m.loss_running, dtype=np.float64),
+         Bcp_final=np.concatenate([A.detach().numpy().reshape(-1) for A in m.Bcp]), converged=np.int32(conv),
+         meta=np.array(json.dumps(meta)))
+
+
+def windowed_case(name, seed, series_shape, win_range, rank, lam, adam_kwargs, iters, n_classes=0):
+    """Windowed data path (util.py:67-98): the reference's WindowedDataset over an untiled series,
+    every usable window materialised in usable_idx order and fitted by the reference's fit_Adam
+    (standard…py:400-476, or multinomial…py:389-471 when n_classes > 0).  The fixture keeps only
+    the untiled series; consumers rebuild the windows (windowed_view / HostStream)."""
+    rng = np.random.default_rng(seed)
+    Sq, S = exact_X(rng, series_shape)
+    T = series_shape[0]
+    if n_classes:
+        ys = rng.integers(0, n_classes, size=T)
+        ys[-win_range[0]:-win_range[0] + n_classes] = np.arange(n_classes)  # every class in a usable window
+        ys_t = torch.tensor(ys)
+    else:
+        ys_t = torch.tensor(rng.standard_normal(T).astype(np.float32))
+    ds = RUTIL.WindowedDataset(S, ys_t, win_range)
+    items = [ds[int(i)] for i in ds.usable_idx]
+    X = torch.stack([a for a, _ in items])
+    y = torch.stack([b for _, b in items])
+    if n_classes:
+        y_np = y.numpy().astype(np.int64)
+        assert len(np.unique(y_np)) == n_classes
+        torch.manual_seed(seed)
+        m = MTR.CP_logistic_regression(X.numpy(), y_np, rank=rank)
+        Bcp0 = [A.detach().numpy().copy() for A in m.Bcp]
+        Sp = MTR.model(m.X, m.Bcp, m.weights, m.non_negative, softplus_kwargs=m.softplus_kwargs)
+        loss = torch.nn.CrossEntropyLoss(weight=torch.ones(n_classes))(Sp, m.y) + lam * MTR.L2_penalty(m.Bcp)
+        loss.backward()
+        grads = [A.grad.numpy().copy() for A in m.Bcp]
+        for A in m.Bcp:
+            A.grad = None
+        torch.manual_seed(seed)
+        m10 = MTR.CP_logistic_regression(X.numpy(), y_np, rank=rank)
+        m10.fit_Adam(lambda_L2=lam, max_iter=min(10, iters), tol=0.0, patience=10, weights=np.ones(n_classes),
+                     verbose=False, Adam_kwargs=dict(adam_kwargs))
+        conv = m.fit_Adam(lambda_L2=lam, max_iter=iters, tol=0.0, patience=10, weights=np.ones(n_classes),
+                          verbose=False, Adam_kwargs=dict(adam_kwargs))
+        extra = dict(probs0=Sp.detach().numpy(), y_series=ys.astype(np.int64))
+        bias = {}
+    else:
+        torch.manual_seed(seed)
+        m = STR.CP_linear_regression(X.shape, rank=rank)
+        Bcp0 = [A.detach().numpy().copy() for A in m.Bcp]
+        b0 = m.bias.detach().numpy().copy()
+        yh = STR.lin_model(X, m.Bcp, m.weights, m.non_negative, m.bias, softplus_kwargs=m.softplus_kwargs)
+        loss = torch.nn.MSELoss()(yh, y) + lam * STR.L2_penalty(m.Bcp)
+        loss.backward()
+        grads = [A.grad.numpy().copy() for A in m.Bcp]
+        bgrad = m.bias.grad.numpy().copy()
+        for A in m.Bcp:
+            A.grad = None
+        m.bias.grad = None
+        torch.manual_seed(seed)
+        m10 = STR.CP_linear_regression(X.shape, rank=rank)
+        m10.fit_Adam(X, y, lambda_L2=lam, max_iter=min(10, iters), tol=0.0, patience=10, verbose=False,
+                     Adam_kwargs=dict(adam_kwargs))
+        conv = m.fit_Adam(X, y, lambda_L2=lam, max_iter=iters, tol=0.0, patience=10, verbose=False,
+                          Adam_kwargs=dict(adam_kwargs))
+        extra = dict(y_hat0=yh.detach().numpy(), y_series=ys_t.numpy(), bias0=b0, bias_grad0=bgrad,
+                     bias_10=m10.bias.detach().numpy().copy(), bias_final=m.bias.detach().numpy().copy())
+    meta = dict(model="windowed_" + ("multinomial" if n_classes else "linear"), seed=seed,
+                series_shape=list(series_shape), win_range=list(win_range), n_windows=len(items),
+                window_shape=list(X.shape[1:]), n_classes=n_classes, rank=rank, lambda_L2=lam,
+                adam_kwargs=adam_kwargs, max_iter=iters, tol=0.0, patience=10,
+                non_negative=list(map(bool, m.non_negative)), softplus_kwargs=m.softplus_kwargs,
+                factor_shapes=[list(a.shape) for a in Bcp0], torch=torch.__version__)
+    save(name, X_q=Sq, Bcp0=np.concatenate([a.reshape(-1) for a in Bcp0]), loss0=np.float64(loss.item()),
+         grads0=np.concatenate([g.reshape(-1) for g in grads]),
+         Bcp_10=np.concatenate([A.detach().numpy().reshape(-1) for A in m10.Bcp]),
+         loss_running_10=np.array(m10.loss_running, dtype=np.float64),
+         loss_running=np.array(m.loss_running, dtype=np.float64),
+         Bcp_final=np.concatenate([A.detach().numpy().reshape(-1) for A in m.Bcp]), converged=np.int32(conv),
+         meta=np.array(json.dumps(meta)), **extra)
 
 
 def _flat(ts):
@@ -287,6 +399,20 @@ def main():
     linear_lbfgs_case("lin_lbfgs", 18, (64, 8, 4), 2, 1e-3, 6,
                       {'lr': 1, 'max_iter': 20, 'max_eval': None, 'tolerance_grad': 1e-07,
                        'tolerance_change': 1e-09, 'history_size': 100, 'line_search_fn': "strong_wolfe"})
+    # BASELINE configs[0]: X (1024, 32, 16), rank 2, planted y, 200 Adam iterations
+    linear_case("lin_cfg1", 41, (1024, 32, 16), 2, [False, False, False], 0.0, 0.01, adam, 200, planted=True)
+    linear_case("lin_cfg1_amsgrad", 41, (1024, 32, 16), 2, [False, False, False], 0.0, 0.01,
+                {'lr': 0.01, 'amsgrad': True}, 200, planted=True)
+    mnl_lbfgs_case("mnllbfgs_basic", 25, (128, 8, 4), 3, 2, [1.0, 1.0, 1.0], 1e-3, 6,
+                   {'lr': 1, 'max_iter': 20, 'max_eval': None, 'tolerance_grad': 1e-07,
+                    'tolerance_change': 1e-09, 'history_size': 100, 'line_search_fn': "strong_wolfe"})
+    # well-conditioned: few inner iterations, no line search -> the fp32 trajectory is reproducible
+    mnl_lbfgs_case("mnllbfgs_weighted", 26, (96, 6, 5), 4, 3, [0.5, 2.0, 1.0, 1.5], 1e-2, 8,
+                   {'lr': 0.05, 'max_iter': 3, 'max_eval': None, 'tolerance_grad': 1e-07,
+                    'tolerance_change': 1e-09, 'history_size': 10, 'line_search_fn': None}, logging_interval=2)
+    windowed_case("win_lin", 51, (300, 12), (-4, 4), 3, 0.01, adam, 50)
+    windowed_case("win_lin_asym", 52, (200, 6, 5), (0, 5), 2, 0.01, {'lr': 0.02, 'amsgrad': True}, 30)
+    windowed_case("win_mnl", 53, (260, 10), (-3, 5), 2, 0.01, adam, 40, n_classes=3)
     mnl_case("mnl_basic", 21, (128, 8, 4), 3, 2, [False, False, False], [1, 1, 1], 0.01, adam, 50)
     mnl_case("mnl_nonneg_weighted_amsgrad", 22, (160, 6, 5), 4, 3, [True, False, True], [0.5, 2.0, 1.0, 1.5], 0.02,
              {'lr': 0.01, 'amsgrad': True}, 50)
