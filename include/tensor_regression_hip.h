@@ -87,7 +87,7 @@ const char* tr_last_error(void);
  *   n_feature_modes K = X.ndim - 1 (1 .. TR_MAX_FACTORS-1)
  *   feature_dims   host array of K dims (I_1 .. I_K)
  *   n_classes      multinomial: C (the extra factor has C rows); linear: ignored (use 1)
- *   rank           R (1 .. 64)
+ *   rank           R (1 .. 1024)
  *   max_rows       largest sample count later passed to tr_loss_grad (sizes the workspace)
  *   non_negative   host array, one flag per factor (K linear / K+1 multinomial): softplus
  *                  is applied to flagged factors (non_neg_fn, standard…py:53-85)

@@ -6,7 +6,7 @@
 
 #define TR_WAVE 64
 #define TR_MAXF 8     // max factors (modes of the dense coefficient tensor)
-#define TR_MAXR 64    // max CP rank
+#define TR_MAXR 1024  // max CP rank (MTTKRP tiles ranks by 64; the reference has no limit)
 // stop-flag value written by k_update when the pass it was about to apply failed on the device
 // (gradient-arena status slot set): TR_STOP_DEVICE_ERROR - iteration.  Distinct from the plateau
 // stop (iterations completed, > 0) and the spectral NaN stop (-(iterations run) > -2^30).
@@ -64,6 +64,16 @@ __device__ __forceinline__ float tr_wave_allreduce(float v) {
   const float a = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
   const float b = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
   return a + b;
+}
+__device__ __forceinline__ float tr_wave_allreduce_max(float v) {
+  v = fmaxf(v, tr_swz_xor<0x401F>(v));
+  v = fmaxf(v, tr_swz_xor<0x201F>(v));
+  v = fmaxf(v, tr_swz_xor<0x101F>(v));
+  v = fmaxf(v, tr_swz_xor<0x081F>(v));
+  v = fmaxf(v, tr_swz_xor<0x041F>(v));
+  const float a = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+  const float b = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+  return fmaxf(a, b);
 }
 __device__ __forceinline__ double tr_wave_allreduce_d(double v) {
 #pragma unroll

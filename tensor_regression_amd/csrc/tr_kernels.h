@@ -8,7 +8,9 @@
 
 namespace tr {
 
-enum { MODE_LIN_TRAIN = 0, MODE_LIN_PRED = 1, MODE_MNL_TRAIN = 2, MODE_MNL_PRED = 3 };
+// MODE_MNL_LOGITS: raw logits Z of one class tile (wide-class path, C > 16: the softmax / CE
+// epilogue then runs in k_softmax_rows over the whole row of C logits)
+enum { MODE_LIN_TRAIN = 0, MODE_LIN_PRED = 1, MODE_MNL_TRAIN = 2, MODE_MNL_PRED = 3, MODE_MNL_LOGITS = 4 };
 
 // Scalars of one k_update launch (Adam constants precomputed on the host in fp64 exactly
 // as torch/optim/adam.py does with python floats, then rounded to fp32 like torch's scalar
@@ -81,6 +83,19 @@ hipError_t launch_rows_mfma(int mode, const float* X, int64_t N, int64_t P, int6
 hipError_t launch_cols(int C, int W, int64_t nstripes, int64_t nchunks, const float* X, int64_t N,
                        int64_t P, int64_t xld, const float* V, int64_t rows_per_chunk, float* gpart, int reverse,
                        const int32_t* stop, hipStream_t st);
+// wide-class multinomial path (any C; C > 16 splits into class tiles of 16):
+//   logits Z (N x C) = X . B by class tile (MFMA when mfma != 0, else VALU), then
+//   k_softmax_rows: double softmax + weighted CE + dZ in place (train) or the probabilities (pred),
+//   then the column reduction X^T dZ by class tile into the (slab, class, feature) partials
+int wide_class_tile(void);
+hipError_t launch_mnl_logits(int C, int mfma, int W, const float* X, int64_t N, int64_t P, int64_t xld,
+                             const float* Bt, float* Z, const int32_t* stop, hipStream_t st);
+int64_t softmax_rows_num_waves(int64_t N);
+hipError_t launch_softmax_rows(int mode, int C, float* Z, int64_t N, const int64_t* lab, const float* class_w,
+                               float scale, float* out, double* dpart, const int32_t* stop, hipStream_t st);
+hipError_t launch_cols_wide(int C, int W, int64_t nstripes, int64_t nchunks, const float* X, int64_t N, int64_t P,
+                            int64_t xld, const float* V, int64_t rows_per_chunk, float* gpart, int reverse,
+                            const int32_t* stop, hipStream_t st);
 hipError_t launch_reduce_slabs(int W, const float* part, int64_t nslabs, int64_t ncols, float* out,
                                const double* dpart, int64_t nd, double loss_scale, float* loss_slot,
                                float* bias_slot, const int32_t* stop, hipStream_t st,

@@ -281,7 +281,7 @@ __global__ __launch_bounds__(256) void k_rows(
     const float* __restrict__ X, int64_t N, int64_t P, int64_t xld, const float* __restrict__ Bt,
     const float* __restrict__ bias_p, const void* __restrict__ target,
     const float* __restrict__ class_w, float scale, float* __restrict__ out,
-    double* __restrict__ dpart, float* __restrict__ yhat, const int32_t* __restrict__ stop) {
+    double* __restrict__ dpart, float* __restrict__ yhat, const int32_t* __restrict__ stop, int64_t ldo) {
   using V = VecT<W>;
   using VT = typename V::T;
   if (stop != nullptr && *stop != 0) return;
@@ -347,7 +347,16 @@ __global__ __launch_bounds__(256) void k_rows(
 #pragma unroll
     for (int c = 0; c < C; ++c) acc[r][c] = tr_wave_allreduce(acc[r][c]);
 
-  if (MODE == MODE_LIN_TRAIN || MODE == MODE_LIN_PRED) {
+  if (MODE == MODE_MNL_LOGITS) {  // one class tile of the logits, row stride ldo
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      const int64_t row = row0 + r;
+      if (row < N)
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+          if (lane == c) out[row * ldo + c] = acc[r][c];
+    }
+  } else if (MODE == MODE_LIN_TRAIN || MODE == MODE_LIN_PRED) {
     const float bias = *bias_p;
     const float* y = reinterpret_cast<const float*>(target);
     double sse = 0.0, rsum = 0.0;
@@ -478,11 +487,16 @@ template <int MODE, int RT>
 __global__ __launch_bounds__(256) void k_rows_mfma(
     const float* __restrict__ X, int64_t N, int64_t P, int64_t xld, const float* __restrict__ Bt, int C,
     const int64_t* __restrict__ lab, const float* __restrict__ class_w, float scale,
-    float* __restrict__ out, double* __restrict__ dpart, const int32_t* __restrict__ stop) {
+    float* __restrict__ out, double* __restrict__ dpart, const int32_t* __restrict__ stop, int64_t ldo) {
   if (stop != nullptr && *stop != 0) return;
   const int lane = threadIdx.x & (TR_WAVE - 1);
   const int64_t gw = (int64_t)blockIdx.x * (blockDim.x / TR_WAVE) + (threadIdx.x / TR_WAVE);
   const int64_t row0 = gw * (16 * RT);
+  if (MODE == MODE_MNL_LOGITS) {  // class tile blockIdx.y: Bt / out are offset by the host
+    Bt += (int64_t)blockIdx.y * 16 * P;
+    out += (int64_t)blockIdx.y * 16;
+    C = C - 16 * (int)blockIdx.y < 16 ? C - 16 * (int)blockIdx.y : 16;
+  }
   const int i = lane & 15;  // A row in tile / class column
   const int g = lane >> 4;  // k group
   if (row0 >= N) {
@@ -547,6 +561,16 @@ __global__ __launch_bounds__(256) void k_rows_mfma(
   }
   const float NEG = -__builtin_huge_valf();
   double lsum = 0.0;
+  if (MODE == MODE_MNL_LOGITS) {
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        const int64_t row = row0 + rt * 16 + 4 * g + reg;
+        if (cls_ok && row < N) out[row * ldo + i] = acc[rt][reg];
+      }
+    return;
+  }
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {
 #pragma unroll
@@ -558,7 +582,7 @@ __global__ __launch_bounds__(256) void k_rows_mfma(
       const float sum = tr_sum16(ez);
       const float S = ez * (1.0f / sum);
       if (MODE == MODE_MNL_PRED) {
-        if (cls_ok && row < N) out[row * C + i] = S;
+        if (cls_ok && row < N) out[row * ldo + i] = S;
         continue;
       }
       // CrossEntropyLoss(weight) on the probabilities S (double softmax)
@@ -573,7 +597,71 @@ __global__ __launch_bounds__(256) void k_rows_mfma(
       if (is_y) lsum += (double)cw * (double)(-((S - m2) - lse));
       const float dS = cls_ok ? (q * (1.0f / s2) - (is_y ? 1.0f : 0.0f)) * (cw * scale) : 0.f;
       const float dot = tr_sum16(dS * S);
-      if (cls_ok && valid) out[row * C + i] = S * (dS - dot);
+      if (cls_ok && valid) out[row * ldo + i] = S * (dS - dot);
+    }
+  }
+  if (MODE == MODE_MNL_TRAIN) {
+    lsum = tr_wave_allreduce_d(lsum);
+    if (lane == 0) {
+      dpart[2 * gw] = lsum;
+      dpart[2 * gw + 1] = 0.0;
+    }
+  }
+}
+
+// ==========================================================================================
+// K2w: wide-class epilogue (C > 16).  One wave per row (grid-stride over rows), the C logits
+// across lanes in chunks of 64: S = softmax(Z) (multinomial…py:187), then CrossEntropyLoss(weight)
+// on the probabilities (the double softmax, :448-456) and dZ = S (dS - <dS, S>), written over Z.
+// Fixed-order reductions (per-lane strided sums, then the wave butterfly): deterministic.
+// ==========================================================================================
+template <int MODE>
+__global__ __launch_bounds__(256) void k_softmax_rows(float* __restrict__ Z, int64_t N, int C,
+                                                      const int64_t* __restrict__ lab,
+                                                      const float* __restrict__ class_w, float scale,
+                                                      float* __restrict__ out, double* __restrict__ dpart,
+                                                      const int32_t* __restrict__ stop) {
+  if (stop != nullptr && *stop != 0) return;
+  const int lane = threadIdx.x & (TR_WAVE - 1);
+  const int64_t gw = (int64_t)blockIdx.x * (blockDim.x / TR_WAVE) + (threadIdx.x / TR_WAVE);
+  const int64_t nw = (int64_t)gridDim.x * (blockDim.x / TR_WAVE);
+  const float NEG = -__builtin_huge_valf();
+  double lsum = 0.0;
+  for (int64_t row = gw; row < N; row += nw) {
+    float* z = Z + row * C;
+    float mx = NEG;
+    for (int c = lane; c < C; c += TR_WAVE) mx = fmaxf(mx, z[c]);
+    mx = tr_wave_allreduce_max(mx);
+    float sum = 0.f;
+    for (int c = lane; c < C; c += TR_WAVE) sum += expf(z[c] - mx);
+    sum = tr_wave_allreduce(sum);
+    const float inv = 1.0f / sum;
+    if (MODE == MODE_MNL_PRED) {
+      for (int c = lane; c < C; c += TR_WAVE) out[row * C + c] = expf(z[c] - mx) * inv;
+      continue;
+    }
+    float m2 = NEG;
+    for (int c = lane; c < C; c += TR_WAVE) m2 = fmaxf(m2, expf(z[c] - mx) * inv);
+    m2 = tr_wave_allreduce_max(m2);
+    float s2 = 0.f;
+    for (int c = lane; c < C; c += TR_WAVE) s2 += expf(expf(z[c] - mx) * inv - m2);
+    s2 = tr_wave_allreduce(s2);
+    const float lse = logf(s2), inv2 = 1.0f / s2;
+    const int64_t yl = lab[row];
+    const float cw = class_w[yl];
+    const float gsc = cw * scale;
+    float dot = 0.f;
+    for (int c = lane; c < C; c += TR_WAVE) {
+      const float S = expf(z[c] - mx) * inv;
+      const float dS = (expf(S - m2) * inv2 - (c == yl ? 1.0f : 0.0f)) * gsc;
+      dot = fmaf(dS, S, dot);
+      if (c == yl) lsum += (double)cw * (double)(-((S - m2) - lse));
+    }
+    dot = tr_wave_allreduce(dot);
+    for (int c = lane; c < C; c += TR_WAVE) {
+      const float S = expf(z[c] - mx) * inv;
+      const float dS = (expf(S - m2) * inv2 - (c == yl ? 1.0f : 0.0f)) * gsc;
+      z[c] = S * (dS - dot);
     }
   }
   if (MODE == MODE_MNL_TRAIN) {
@@ -596,7 +684,7 @@ template <int C, int CW, int W>
 __global__ __launch_bounds__(256) void k_cols(const float* __restrict__ X, int64_t N, int64_t P, int64_t xld,
                                               const float* __restrict__ Vw, int64_t rows_per_chunk,
                                               float* __restrict__ gpart, int reverse,
-                                              const int32_t* __restrict__ stop) {
+                                              const int32_t* __restrict__ stop, int64_t ldv, int64_t slab_stride) {
   using V = VecT<W>;
   using VT = typename V::T;
   if (stop != nullptr && *stop != 0) return;
@@ -633,7 +721,7 @@ __global__ __launch_bounds__(256) void k_cols(const float* __restrict__ X, int64
     for (int u = 0; u < U; ++u) {
 #pragma unroll
       for (int c = 0; c < C; ++c) {
-        const float v = Vw[(n + u) * C + c];
+        const float v = Vw[(n + u) * ldv + c];
 #pragma unroll
         for (int j = 0; j < CW; ++j) V::axpy(v, x[u][j], acc[j][c]);
       }
@@ -645,12 +733,12 @@ __global__ __launch_bounds__(256) void k_cols(const float* __restrict__ X, int64
     for (int j = 0; j < CW; ++j) x[j] = ldx(Xv + n * LDW + col[j]);
 #pragma unroll
     for (int c = 0; c < C; ++c) {
-      const float v = Vw[n * C + c];
+      const float v = Vw[n * ldv + c];
 #pragma unroll
       for (int j = 0; j < CW; ++j) V::axpy(v, x[j], acc[j][c]);
     }
   }
-  VT* gp = reinterpret_cast<VT*>(gpart + k * C * P);
+  VT* gp = reinterpret_cast<VT*>(gpart + k * slab_stride);
 #pragma unroll
   for (int j = 0; j < CW; ++j)
     if (ok[j])
@@ -767,6 +855,9 @@ __global__ __launch_bounds__(256) void k_mttkrp(FactorSet fs, const float* __res
   if (stop != nullptr && *stop != 0) return;
   const int R = fs.rank;
   const int nf = fs.nf;
+  // rank tile of this workgroup: columns [rt0, rt0 + Rt) (grid.y tiles a rank beyond RMAX)
+  const int rt0 = (int)blockIdx.y * RMAX;
+  const int Rt = R - rt0 < RMAX ? R - rt0 : RMAX;
   int b = blockIdx.x;
   int f = 0;
   while (f < nf - 1 && b >= (int)fs.dim[f]) {
@@ -789,7 +880,7 @@ __global__ __launch_bounds__(256) void k_mttkrp(FactorSet fs, const float* __res
     }
     F = sphi;
   }
-  if (threadIdx.x < RMAX) sw[threadIdx.x] = threadIdx.x < R ? w[threadIdx.x] : 0.f;
+  if (threadIdx.x < RMAX) sw[threadIdx.x] = (int)threadIdx.x < Rt ? w[rt0 + threadIdx.x] : 0.f;
   __syncthreads();
 
   // other modes ordered by decreasing dense stride (digit NO-1 = most contiguous), host-sorted
@@ -853,7 +944,7 @@ __global__ __launch_bounds__(256) void k_mttkrp(FactorSet fs, const float* __res
 #pragma unroll
       for (int k = 0; k < NOD; ++k) {
         pos += idx[k] * ostr[k];
-        frow[u][k] = ooff[k] + idx[k] * S;
+        frow[u][k] = ooff[k] + idx[k] * S + rt0;
       }
       gv[u] = ok ? G[pos] : 0.f;
       advance();
@@ -862,7 +953,7 @@ __global__ __launch_bounds__(256) void k_mttkrp(FactorSet fs, const float* __res
     for (int u = 0; u < U; ++u) {
 #pragma unroll
       for (int r = 0; r < RMAX; ++r) {
-        if (r < R) {
+        if (r < Rt) {
           float prod = sw[r];
 #pragma unroll
           for (int k = 0; k < NO; ++k) prod *= F[frow[u][k] + r];
@@ -875,16 +966,16 @@ __global__ __launch_bounds__(256) void k_mttkrp(FactorSet fs, const float* __res
   const int q = threadIdx.x / TR_WAVE;
 #pragma unroll
   for (int r = 0; r < RMAX; ++r) {
-    if (r < R) {
+    if (r < Rt) {
       const float v = tr_wave_allreduce(acc[r]);
       if (lane == 0) red[q][r] = v;
     }
   }
   __syncthreads();
-  if (threadIdx.x < R) {
+  if ((int)threadIdx.x < Rt) {
     const int r = threadIdx.x;
     const float s2 = ((red[0][r] + red[1][r]) + red[2][r]) + red[3][r];
-    const int64_t e = fs.off[f] + (int64_t)i * R + r;
+    const int64_t e = fs.off[f] + (int64_t)i * R + rt0 + r;
     out[e] = s2 * dphi[e];
   }
 }
@@ -1186,7 +1277,7 @@ static hipError_t rows_launch_t(const float* X, int64_t N, int64_t P, int64_t xl
   const int64_t waves = (N + RB - 1) / RB;
   const unsigned grid = cdiv(waves, 4);
   hipLaunchKernelGGL((k_rows<C, RB, MODE, W>), dim3(grid), dim3(256), 0, st, X, N, P, xld, Bt, bias, target,
-                     class_w, scale, out, dpart, yhat, stop);
+                     class_w, scale, out, dpart, yhat, stop, (int64_t)C);
   return hipGetLastError();
 }
 
@@ -1236,10 +1327,10 @@ hipError_t launch_rows_mfma(int mode, const float* X, int64_t N, int64_t P, int6
   const unsigned grid = cdiv(waves, 4);
   if (mode == MODE_MNL_TRAIN)
     hipLaunchKernelGGL((k_rows_mfma<MODE_MNL_TRAIN, kMfmaRT>), dim3(grid), dim3(256), 0, st, X, N, P, xld, Bt, C, lab,
-                       class_w, scale, out, dpart, stop);
+                       class_w, scale, out, dpart, stop, (int64_t)C);
   else if (mode == MODE_MNL_PRED)
     hipLaunchKernelGGL((k_rows_mfma<MODE_MNL_PRED, kMfmaRT>), dim3(grid), dim3(256), 0, st, X, N, P, xld, Bt, C, lab,
-                       class_w, scale, out, dpart, stop);
+                       class_w, scale, out, dpart, stop, (int64_t)C);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();
@@ -1249,10 +1340,10 @@ hipError_t launch_rows_mfma(int mode, const float* X, int64_t N, int64_t P, int6
 template <int C, int W>
 static hipError_t cols_launch_t(int64_t nstripes, int64_t nchunks, const float* X, int64_t N, int64_t P, int64_t xld,
                                 const float* V, int64_t rpc, float* gpart, int reverse,
-                                const int32_t* stop, hipStream_t st) {
+                                const int32_t* stop, hipStream_t st, int64_t ldv = C, int64_t slab_stride = -1) {
   constexpr int CW = (C == 1) ? 4 : (C == 2 ? 2 : 1);
   hipLaunchKernelGGL((k_cols<C, CW, W>), dim3((unsigned)nstripes, (unsigned)nchunks), dim3(256), 0, st,
-                     X, N, P, xld, V, rpc, gpart, reverse, stop);
+                     X, N, P, xld, V, rpc, gpart, reverse, stop, ldv, slab_stride < 0 ? (int64_t)C * P : slab_stride);
   return hipGetLastError();
 }
 
@@ -1265,6 +1356,98 @@ hipError_t launch_cols(int C, int W, int64_t nstripes, int64_t nchunks, const fl
   TR_C_CASES(TR_CALL_COLS)
 #undef TR_CALL_COLS
   return hipErrorInvalidValue;
+}
+
+// ---- wide-class multinomial path (C > 16) ------------------------------------------------------
+int wide_class_tile(void) { return 16; }
+
+template <int CT, int W>
+static hipError_t logits_tile_t(const float* X, int64_t N, int64_t P, int64_t xld, const float* Bt, float* Z,
+                                int64_t ldo, const int32_t* stop, hipStream_t st) {
+  const int64_t waves = (N + 3) / 4;
+  hipLaunchKernelGGL((k_rows<CT, 4, MODE_MNL_LOGITS, W>), dim3(cdiv(waves, 4)), dim3(256), 0, st, X, N, P, xld, Bt,
+                     nullptr, nullptr, nullptr, 0.f, Z, nullptr, nullptr, stop, ldo);
+  return hipGetLastError();
+}
+
+hipError_t launch_mnl_logits(int C, int mfma, int W, const float* X, int64_t N, int64_t P, int64_t xld,
+                             const float* Bt, float* Z, const int32_t* stop, hipStream_t st) {
+  const int ntiles = (C + 15) / 16;
+  if (mfma) {  // every class tile in one launch (grid.y); Bt padded to 16 * ntiles class rows
+    if (P % 32 != 0) return hipErrorInvalidValue;
+    const int64_t waves = rows_mfma_num_waves(N);
+    hipLaunchKernelGGL((k_rows_mfma<MODE_MNL_LOGITS, kMfmaRT>), dim3(cdiv(waves, 4), (unsigned)ntiles), dim3(256), 0,
+                       st, X, N, P, xld, Bt, C, nullptr, nullptr, 0.f, Z, nullptr, stop, (int64_t)C);
+    return hipGetLastError();
+  }
+  for (int t = 0; t < ntiles; ++t) {
+    const int CT = C - 16 * t < 16 ? C - 16 * t : 16;
+    const float* Bt_t = Bt + (int64_t)16 * t * P;
+    float* Z_t = Z + 16 * t;
+    hipError_t e = hipErrorInvalidValue;
+#define TR_CALL_LOGITS(CC) \
+  (W == 4 ? logits_tile_t<CC, 4>(X, N, P, xld, Bt_t, Z_t, C, stop, st) : logits_tile_t<CC, 1>(X, N, P, xld, Bt_t, Z_t, C, stop, st))
+    switch (CT) {
+      case 1: e = TR_CALL_LOGITS(1); break;   case 2: e = TR_CALL_LOGITS(2); break;
+      case 3: e = TR_CALL_LOGITS(3); break;   case 4: e = TR_CALL_LOGITS(4); break;
+      case 5: e = TR_CALL_LOGITS(5); break;   case 6: e = TR_CALL_LOGITS(6); break;
+      case 7: e = TR_CALL_LOGITS(7); break;   case 8: e = TR_CALL_LOGITS(8); break;
+      case 9: e = TR_CALL_LOGITS(9); break;   case 10: e = TR_CALL_LOGITS(10); break;
+      case 11: e = TR_CALL_LOGITS(11); break; case 12: e = TR_CALL_LOGITS(12); break;
+      case 13: e = TR_CALL_LOGITS(13); break; case 14: e = TR_CALL_LOGITS(14); break;
+      case 15: e = TR_CALL_LOGITS(15); break; default: e = TR_CALL_LOGITS(16); break;
+    }
+#undef TR_CALL_LOGITS
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+static const int64_t kSoftmaxWaves = 4096;
+int64_t softmax_rows_num_waves(int64_t N) { return N < kSoftmaxWaves ? (N > 0 ? N : 1) : kSoftmaxWaves; }
+
+hipError_t launch_softmax_rows(int mode, int C, float* Z, int64_t N, const int64_t* lab, const float* class_w,
+                               float scale, float* out, double* dpart, const int32_t* stop, hipStream_t st) {
+  const int64_t waves = softmax_rows_num_waves(N);
+  const unsigned grid = cdiv(waves, 4);  // 4 waves per workgroup; dpart holds 4 * grid entries
+  if (mode == MODE_MNL_TRAIN)
+    hipLaunchKernelGGL(k_softmax_rows<MODE_MNL_TRAIN>, dim3(grid), dim3(256), 0, st, Z, N, C, lab, class_w, scale,
+                       out, dpart, stop);
+  else if (mode == MODE_MNL_PRED)
+    hipLaunchKernelGGL(k_softmax_rows<MODE_MNL_PRED>, dim3(grid), dim3(256), 0, st, Z, N, C, lab, class_w, scale,
+                       out, dpart, stop);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t launch_cols_wide(int C, int W, int64_t nstripes, int64_t nchunks, const float* X, int64_t N, int64_t P,
+                            int64_t xld, const float* V, int64_t rows_per_chunk, float* gpart, int reverse,
+                            const int32_t* stop, hipStream_t st) {
+  // class tiles of 16: X is read once per tile; the slabs keep the (class, feature) layout of C
+  for (int t = 0; t * 16 < C; ++t) {
+    const int CT = C - 16 * t < 16 ? C - 16 * t : 16;
+    const float* Vt = V + 16 * t;
+    float* gt = gpart + (int64_t)16 * t * P;
+    const int64_t ss = (int64_t)C * P;
+    hipError_t e = hipErrorInvalidValue;
+#define TR_CALL_COLSW(CC)                                                                                   \
+  (W == 4 ? cols_launch_t<CC, 4>(nstripes, nchunks, X, N, P, xld, Vt, rows_per_chunk, gt, reverse, stop, st, C, ss) \
+          : cols_launch_t<CC, 1>(nstripes, nchunks, X, N, P, xld, Vt, rows_per_chunk, gt, reverse, stop, st, C, ss))
+    switch (CT) {
+      case 1: e = TR_CALL_COLSW(1); break;   case 2: e = TR_CALL_COLSW(2); break;
+      case 3: e = TR_CALL_COLSW(3); break;   case 4: e = TR_CALL_COLSW(4); break;
+      case 5: e = TR_CALL_COLSW(5); break;   case 6: e = TR_CALL_COLSW(6); break;
+      case 7: e = TR_CALL_COLSW(7); break;   case 8: e = TR_CALL_COLSW(8); break;
+      case 9: e = TR_CALL_COLSW(9); break;   case 10: e = TR_CALL_COLSW(10); break;
+      case 11: e = TR_CALL_COLSW(11); break; case 12: e = TR_CALL_COLSW(12); break;
+      case 13: e = TR_CALL_COLSW(13); break; case 14: e = TR_CALL_COLSW(14); break;
+      case 15: e = TR_CALL_COLSW(15); break; default: e = TR_CALL_COLSW(16); break;
+    }
+#undef TR_CALL_COLSW
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 // ---- slab reduction --------------------------------------------------------------------------
@@ -1314,7 +1497,7 @@ hipError_t launch_mttkrp(const FactorSet& fs, const float* phi, const float* dph
   const int64_t padded = rows * (fs.rank | 1);  // odd LDS row stride (k_mttkrp)
   const int use_lds = padded <= kLdsFactorLimit;
   const size_t lds = use_lds ? (size_t)padded * sizeof(float) : 0;
-  const dim3 grid((unsigned)rows);
+  const dim3 grid((unsigned)rows, (unsigned)((fs.rank + 63) / 64));  // rank tiles of 64 beyond rank 64
   if (fs.rank <= 8) return mttkrp_launch_r<8>(fs, phi, dphi, w, G, grad, use_lds, stop, st, grid, lds);
   if (fs.rank <= 16) return mttkrp_launch_r<16>(fs, phi, dphi, w, G, grad, use_lds, stop, st, grid, lds);
   if (fs.rank <= 32) return mttkrp_launch_r<32>(fs, phi, dphi, w, G, grad, use_lds, stop, st, grid, lds);

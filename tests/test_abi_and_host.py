@@ -39,7 +39,8 @@ def test_argument_validation_without_gpu():
     assert lib.tr_plan_create(ctypes.byref(h), 0, 0, 0, dims, 1, 2, 10, nn, 50.0, 1.0) == -1
     assert b"factors" in lib.tr_last_error()
     assert lib.tr_plan_create(ctypes.byref(h), 0, 0, 2, dims, 1, 0, 10, nn, 50.0, 1.0) == -1
-    assert lib.tr_plan_create(ctypes.byref(h), 0, 1, 2, dims, 17, 2, 10, nn, 50.0, 1.0) == -2
+    assert lib.tr_plan_create(ctypes.byref(h), 0, 0, 2, dims, 1, 1025, 10, nn, 50.0, 1.0) == -1  # rank > 1024
+    assert lib.tr_plan_create(ctypes.byref(h), 0, 1, 2, dims, 0, 2, 10, nn, 50.0, 1.0) == -1  # no classes
     assert lib.tr_plan_create(ctypes.byref(h), 0, 7, 2, dims, 1, 2, 10, nn, 50.0, 1.0) == -1
     assert lib.tr_loss_grad(None, None, 0, None, None, 1.0, None, None, None, None, None, None) == -1
     assert lib.tr_adam_step(None, None, None, None, None, None, 0.0, 0.0, 0.9, 0.999, 1e-8, 0.0, 0, 1, None,

@@ -292,6 +292,8 @@ LIN_SHAPES = [
     ((300, 64, 64, 32), 16),   # config-4 row (P = 131072 > LDS): cluster single pass, 5 slices
     ((77, 45000), 3),          # one wide mode: 2-slice cluster, ragged last slice
     ((2, 200, 332), 4),        # N < number of clusters: most clusters own no rows
+    ((90, 10, 10), 65),        # rank beyond 64: MTTKRP rank tiles of 64
+    ((50, 6, 5, 4), 200),      # 4 rank tiles, 3 feature modes
 ]
 
 
@@ -333,7 +335,11 @@ MNL_SHAPES = [((50, 8, 4), 2, 2), ((200, 16, 8), 10, 4), ((97, 5, 7), 16, 3), ((
               # factored single pass: ragged 64-blocks, R % 4 != 0, k ranges split over 2 blocks,
               # fewer samples than workgroups, the config-3 sample shape, one class
               ((300, 100, 12), 7, 5), ((257, 64, 128), 4, 8), ((100, 128, 64), 10, 8), ((700, 72, 40), 3, 3),
-              ((90, 8, 8), 1, 2)]
+              ((90, 8, 8), 1, 2),
+              # wide classes (C > 16): logits by class tile (MFMA when P % 32 == 0, else VALU),
+              # k_softmax_rows, tiled column reduction; rank beyond 64 (MTTKRP rank tiles)
+              ((150, 8, 4), 17, 3), ((230, 16, 8), 40, 5), ((99, 5, 7), 33, 2), ((200, 12), 100, 4),
+              ((120, 6, 5), 5, 70), ((80, 4, 8), 20, 130)]
 
 
 @pytest.mark.parametrize("kind", ["auto", "spi1", "twopass", "valu"])
