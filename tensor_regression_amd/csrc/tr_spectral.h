@@ -37,6 +37,9 @@ struct SpecGeom {
   int nonneg[3];
   // LDS carve (floats)
   int oT, oTail, oRed, oSm, oAcc, oPhi, lds_floats;
+  // generic path (tr_spectral_gen.hip) for shapes outside the fused kernel's envelope
+  int gen;  // 1: T_n staged through HBM by k_specg_fwd / k_specg_epi / k_specg_bwd
+  int gKP;  // K padded to 16 (row stride of the T / dT staging buffer)
 };
 
 // Fills g; returns false (with a reason) when the shape is outside the kernels' envelope.
@@ -59,6 +62,15 @@ hipError_t launch_spec_fused(int mode, const SpecGeom& g, int grid, const float*
                              const float* Phi0, const float* wts, const float* y, float scale, float* slab,
                              int64_t slab_stride, double* dpart, float* out, int64_t rows_per_wg, int reverse,
                              const int32_t* stop, hipStream_t st);
+// generic path: dynamic-LDS attribute of the epilogue kernel; T is a (N x D x gKP) staging buffer;
+// SPEC_TRAIN writes one arena-layout slab (phi space) + (sse, 0) per chunk of ceil(N / nchunks)
+// samples, i.e. ceil(N / ceil(N / nchunks)) slabs
+size_t specg_epi_lds_bytes(const SpecGeom& g);
+hipError_t specg_prepare(const SpecGeom& g);
+hipError_t launch_specg(int mode, const SpecGeom& g, int nchunks, const float* X, int64_t N, int64_t xld,
+                        const float* phi, const float* Phi0, const float* wts, const float* y, float scale,
+                        float* T, float* slab, int64_t slab_stride, double* dpart, float* out,
+                        const int32_t* stop, hipStream_t st);
 // grad[e] = G[e] * dphi[e]  (softplus chain of the reduced phi-space gradient)
 hipError_t launch_spec_chain(int64_t n, const float* G, const float* dphi, float* grad, const int32_t* stop,
                              hipStream_t st);

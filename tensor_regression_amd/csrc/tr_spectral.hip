@@ -17,6 +17,7 @@
 // flight in registers.  The reference makes ≈6 passes over X (permute copy, bmm, norm, ...).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <type_traits>
 
@@ -794,18 +795,18 @@ bool spec_geom_init(SpecGeom* g, int64_t W, int64_t D, int64_t NO, int Rn, int R
     *why = "rank_normal + rank_spectral must be >= 1";
     return false;
   }
-  if (K > 32) {
-    *why = "rank_normal + rank_spectral*(n_complex_dim+1) > 32 is outside the gfx950 spectral kernel envelope";
+  if (K > 256) {
+    *why = "rank_normal + rank_spectral*(n_complex_dim+1) > 256 is outside the gfx950 spectral kernels";
     return false;
   }
-  if (W > 256 || D > 256) {
-    *why = "X.shape[1] > 256 or X.shape[2] > 256 is outside the gfx950 spectral kernel envelope";
+  if (W > (1 << 24) || D > (1 << 16) || NO > (1 << 16)) {
+    *why = "spectral dims out of range";
     return false;
   }
-  if (NO > 256) {
-    *why = "more than 256 outputs is outside the gfx950 spectral kernel envelope";
-    return false;
-  }
+  // the fused single-pass kernel holds one sample + scratch in a CU's LDS; beyond that (or when
+  // forced) the generic path stages T_n through HBM (tr_spectral_gen.hip)
+  const char* force = std::getenv("TR_SPEC_GENERIC");
+  bool fused_ok = K <= 32 && W <= 256 && D <= 256 && NO <= 256 && !(force != nullptr && force[0] == '1');
   g->W = (int)W;
   g->D = (int)D;
   g->NO = (int)NO;
@@ -856,9 +857,16 @@ bool spec_geom_init(SpecGeom* g, int64_t W, int64_t D, int64_t NO, int Rn, int R
   g->oPhi = g->oAcc + AccF;
   const int PhiF = round4((D + NO) * (int64_t)(Rn + Rs) + NO + Rn + Rs);
   g->lds_floats = g->oPhi + PhiF;
-  if ((int64_t)g->lds_floats * 4 > 160 * 1024) {
-    *why = "one sample of X (X.shape[1] * X.shape[2] floats) plus scratch exceeds the 160 KiB LDS of a CU";
-    return false;
+  if (fused_ok && (int64_t)g->lds_floats * 4 > 160 * 1024) fused_ok = false;
+  g->gKP = 16 * cdiv_i(K, 16);
+  g->gen = fused_ok ? 0 : 1;
+  if (g->gen) {
+    g->KT = g->gKP / 16;
+    if (specg_epi_lds_bytes(*g) > 160 * 1024 - 256) {  // (+ the kernel's static loss scratch)
+      *why = "the spectral epilogue of one sample (X.shape[2] * (K + 1) + (X.shape[2] + n_out) * (rank_normal + "
+             "rank_spectral) floats) exceeds the 160 KiB LDS of a CU";
+      return false;
+    }
   }
   return true;
 }
@@ -907,6 +915,10 @@ static const void* spec_kernel_for(const SpecGeom& g, int mode) { return spec_di
 
 hipError_t spec_prepare(const SpecGeom& g, int mode, int* ok) {
   *ok = 0;
+  if (g.gen) {
+    *ok = 1;
+    return mode == SPEC_TRAIN ? specg_prepare(g) : hipSuccess;
+  }
   const void* k = spec_kernel_for(g, mode);
   hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, g.lds_floats * 4);
   if (e != hipSuccess) return e;

@@ -13,8 +13,11 @@ lin_model + spectral_model (norm AFTER the full contraction); the bias is added 
 the spectral fit_Adam / fit stop on a NaN loss.
 
 Deliberate differences: tensors run on a HIP device, fp32 only; a y with n_out == 1 is
-rejected (the reference broadcasts (N,) + (N,1) to (N,N), Q10); the kernel envelope is
-X.shape[1], X.shape[2] <= 256, rank_normal + rank_spectral*(n_complex_dim+1) <= 32.
+rejected (the reference broadcasts (N,) + (N,1) to (N,N), Q10).  Shapes within X.shape[1],
+X.shape[2], n_out <= 256 and K = rank_normal + rank_spectral*(n_complex_dim+1) <= 32 run the
+single-pass kernel (csrc/tr_spectral.hip); larger ones the three-kernel path
+(csrc/tr_spectral_gen.hip) up to K <= 256 and one sample's epilogue (X.shape[2]*(K+1) +
+(X.shape[2]+n_out)*(rank_normal+rank_spectral) floats) within a CU's 160 KiB LDS.
 """
 import numpy as np
 import torch

@@ -142,10 +142,9 @@ def test_spectral_plan_validation_without_gpu():
     # rank_normal + rank_spectral == 0, negative dims: argument errors
     assert lib.tr_plan_create_spectral(ctypes.byref(h), 0, 8, 5, 2, 0, 0, 2, 10, nn, 50.0, 1.0) == -1
     assert lib.tr_plan_create_spectral(ctypes.byref(h), 0, 0, 5, 2, 1, 1, 2, 10, nn, 50.0, 1.0) == -1
-    # outside the kernel envelope: K > 32, W > 256, one sample beyond LDS
-    assert lib.tr_plan_create_spectral(ctypes.byref(h), 0, 8, 5, 2, 8, 13, 2, 10, nn, 50.0, 1.0) == -2
-    assert lib.tr_plan_create_spectral(ctypes.byref(h), 0, 300, 5, 2, 2, 2, 2, 10, nn, 50.0, 1.0) == -2
-    assert lib.tr_plan_create_spectral(ctypes.byref(h), 0, 256, 256, 2, 2, 2, 2, 10, nn, 50.0, 1.0) == -2
+    # outside both spectral paths: K = 8 + 100*3 > 256; one sample's epilogue beyond LDS (D = 5000)
+    assert lib.tr_plan_create_spectral(ctypes.byref(h), 0, 8, 5, 2, 8, 100, 3, 10, nn, 50.0, 1.0) == -2
+    assert lib.tr_plan_create_spectral(ctypes.byref(h), 0, 8, 5000, 2, 4, 4, 2, 10, nn, 50.0, 1.0) == -2
     assert b"LDS" in lib.tr_last_error()
 
 

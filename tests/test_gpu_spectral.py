@@ -1,5 +1,6 @@
 """GPU parity of the spectral model (tensor_regression_amd.spectral_tensor_regression, kernels in
-csrc/tr_spectral.hip) against the reference's golden fixtures (tests/golden/spec_*.npz) and the
+csrc/tr_spectral.hip and, for shapes beyond its LDS envelope, csrc/tr_spectral_gen.hip — forced
+with TR_SPEC_GENERIC=1 to run the fixtures through it too) against the reference's golden fixtures (tests/golden/spec_*.npz) and the
 oracle's fp64 closed form (oracle.cp_oracle.closed_form_spectral).
 
 Tolerances (fp32; north_star: 1e-5 relative on the learned factors and the loss trajectory):
@@ -9,11 +10,32 @@ Tolerances (fp32; north_star: 1e-5 relative on the learned factors and the loss 
   * full horizons: loss_running rel <= 1e-5, same length / convergence flag; factors within
     1e-5 of the reference or no further from the fp64 restatement than the reference is (x2)
 """
+import contextlib
+import os
+
 import numpy as np
 import pytest
 import torch
 
 from golden_util import load_spectral, names, normwise_rel
+
+
+@contextlib.contextmanager
+def spec_path(kind):
+    """'fused': the plan's own choice (the single-pass kernel inside its envelope); 'generic':
+    force the three-kernel path (TR_SPEC_GENERIC=1, read at plan creation)."""
+    from tensor_regression_amd import spectral_tensor_regression as SP
+    old = os.environ.pop("TR_SPEC_GENERIC", None)
+    if kind == "generic":
+        os.environ["TR_SPEC_GENERIC"] = "1"
+    SP._plan_cache.clear()
+    try:
+        yield
+    finally:
+        os.environ.pop("TR_SPEC_GENERIC", None)
+        if old is not None:
+            os.environ["TR_SPEC_GENERIC"] = old
+        SP._plan_cache.clear()
 
 pytestmark = pytest.mark.gpu
 
@@ -58,13 +80,20 @@ def _as_accurate_as_reference(ours, ref32, ref64, tol=RTOL, slack=2.0):
         assert normwise_rel(a, c) <= slack * normwise_rel(b, c) + tol, (e_ref, a.shape)
 
 
+@pytest.mark.parametrize("kind", ["fused", "generic"])
 @pytest.mark.parametrize("name", SPEC)
-def test_spectral_golden(name):
+def test_spectral_golden(name, kind):
+    with spec_path(kind):
+        _spectral_golden(name, kind)
+
+
+def _spectral_golden(name, kind):
     d = load_spectral(name)
     m = d["meta"]
     X = d["X"].to(DEV)
     y = torch.tensor(d["y"], device=DEV)
     model = _model_from(d)
+    assert ("generic" in model._get_plan(X, X.shape[0]).describe) == (kind == "generic")
     # predict() = lin_model + spectral_model (spectral…py:959-960)
     _close(model.predict(X).numpy(), d["predict0"])
     # one forward + loss + gradient (fit model, spectral…py:716-720)
@@ -152,10 +181,25 @@ SHAPES = [
     (77, 17, 7, 2, 0, 4, 1, [False, False, False]),       # rank_normal = 0
     (77, 17, 7, 2, 3, 0, 1, [False, False, False]),       # rank_spectral = 0
 ]
+# beyond the fused kernel's envelope: the generic path whatever TR_SPEC_GENERIC says
+WIDE_SHAPES = [
+    (40, 300, 257, 3, 4, 5, 1, [False, True, False]),     # W > 256 and D > 256
+    (50, 64, 40, 2, 8, 16, 1, [False, False, False]),     # K = 8 + 16*2 = 40 > 32
+    (30, 20, 9, 300, 3, 2, 1, [True, False, False]),      # n_out = 300 > 256
+    (20, 520, 33, 2, 2, 3, 3, [False, False, True]),      # W = 520, Cc = 4
+]
 
 
-@pytest.mark.parametrize("N,W,D,O,Rn,Rs,ncd,nn", SHAPES)
-def test_spectral_shapes_vs_closed_form(N, W, D, O, Rn, Rs, ncd, nn):
+@pytest.mark.parametrize("kind", ["fused", "generic"])
+@pytest.mark.parametrize("N,W,D,O,Rn,Rs,ncd,nn", SHAPES + WIDE_SHAPES)
+def test_spectral_shapes_vs_closed_form(N, W, D, O, Rn, Rs, ncd, nn, kind):
+    if kind == "fused" and (N, W, D, O, Rn, Rs, ncd, nn) in WIDE_SHAPES:
+        pytest.skip("beyond the fused envelope: covered by the generic case")
+    with spec_path(kind):
+        _spectral_shape(N, W, D, O, Rn, Rs, ncd, nn, kind)
+
+
+def _spectral_shape(N, W, D, O, Rn, Rs, ncd, nn, kind):
     from oracle import cp_oracle
     g = torch.Generator().manual_seed(N + W + D)
     X = torch.randn(N, W, D, generator=g)
@@ -172,6 +216,8 @@ def test_spectral_shapes_vs_closed_form(N, W, D, O, Rn, Rs, ncd, nn):
     model.bias = bias.to(DEV)
     Xd, yd = X.to(DEV), y.to(DEV)
     plan = model._get_plan(Xd, N)
+    wide = W > 256 or D > 256 or O > 256 or Rn + Rs * (ncd + 1) > 32
+    assert ("generic" in plan.describe) == (kind == "generic" or wide), plan.describe
     arena = plan.pack(model.Bcp_n, model.Bcp_c, model.bias)
     w = torch.ones(Rn + Rs, device=DEV)
     grad = torch.zeros(plan.num_grads, device=DEV)
@@ -204,7 +250,13 @@ def test_spectral_shapes_vs_closed_form(N, W, D, O, Rn, Rs, ncd, nn):
         assert normwise_rel(lat, ref_lat) <= RTOL
 
 
-def test_spectral_bitwise_reproducible_and_sharded_sum():
+@pytest.mark.parametrize("kind", ["fused", "generic"])
+def test_spectral_bitwise_reproducible_and_sharded_sum(kind):
+    with spec_path(kind):
+        _spectral_bitwise(kind)
+
+
+def _spectral_bitwise(kind):
     N, W, D, O = 1000, 256, 129, 2
     g = torch.Generator().manual_seed(5)
     X = torch.randn(N, W, D, generator=g).to(DEV)
@@ -237,11 +289,17 @@ def test_spectral_bitwise_reproducible_and_sharded_sum():
 
 def test_spectral_envelope_errors():
     from tensor_regression_amd.spectral_tensor_regression import CP_linear_regression
-    X = torch.zeros(4, 300, 10, device=DEV)
+    # K = 10 + 100 * 3 > 256 columns: outside both paths
+    X = torch.zeros(4, 30, 10, device=DEV)
     y = torch.zeros(4, 2, device=DEV)
-    m = CP_linear_regression(X.shape, y.shape, rank_normal=2, rank_spectral=2, device=DEV)
-    with pytest.raises(ValueError, match="envelope"):
+    m = CP_linear_regression(X.shape, y.shape, rank_normal=10, rank_spectral=100, n_complex_dim=2, device=DEV)
+    with pytest.raises(ValueError, match="rank_normal"):
         m.fit_Adam(X, y, max_iter=1, Adam_kwargs={'lr': 0.01})
+    # one sample's epilogue beyond a CU's LDS (D * (K + 1) floats)
+    X = torch.zeros(2, 8, 5000, device=DEV)
+    m = CP_linear_regression(X.shape, y[:2].shape, rank_normal=4, rank_spectral=4, device=DEV)
+    with pytest.raises(ValueError, match="LDS"):
+        m.fit_Adam(X, y[:2], max_iter=1, Adam_kwargs={'lr': 0.01})
     m = CP_linear_regression((4, 8, 5), (4, 1), rank_normal=2, rank_spectral=2, device=DEV)
     with pytest.raises(NotImplementedError):
         m.fit_Adam(torch.zeros(4, 8, 5, device=DEV), torch.zeros(4, 1, device=DEV), max_iter=1,
