@@ -120,10 +120,14 @@ def host_cpu_info():
 
 def cpu_baseline(cfg, X, y, model_init, budget_s=15.0, threads=None):
     """Oracle (reference op sequence on torch CPU) on the same X: 2 warm-up + >= 5 timed
-    iterations at the full per-GPU size, on every core this process may run on."""
+    iterations at the full per-GPU size.  Threads: the host's CPU quota for this
+    job (OMP_NUM_THREADS, which the GPU pool sets to this box's share of the host) or, without
+    one, every CPU in the affinity mask.  On the pool's boxes the mask shows all 256 CPUs of a
+    host shared with other jobs: 256 threads measured 4x (c2) to 10x (c3) slower than 16."""
     from oracle import cp_oracle
     info = host_cpu_info()
-    nthreads = threads or info["affinity_cpus"]
+    quota = os.environ.get("OMP_NUM_THREADS")
+    nthreads = threads or (int(quota) if quota and quota.isdigit() else info["affinity_cpus"])
     torch.set_num_threads(nthreads)
     Xc = X.cpu()
     yc = y.cpu()
@@ -147,15 +151,22 @@ def cpu_baseline(cfg, X, y, model_init, budget_s=15.0, threads=None):
     t1 = time.perf_counter()
     per = max((t1 - t0) / 2, 1e-3)
     iters = int(max(5, min(200, budget_s / per)))
-    t0 = time.perf_counter()
-    run(iters)
-    el = time.perf_counter() - t0
+    log(f"cpu baseline: {nthreads} threads, {per:.2f} s/iteration, timing {iters} iterations")
+    el = 0.0
+    done = 0
+    while done < iters:  # chunks of <= 5 iterations, a progress line after each (long configs)
+        k = min(5, iters - done)
+        t0 = time.perf_counter()
+        run(k)
+        el += time.perf_counter() - t0
+        done += k
+        log(f"cpu baseline: {done}/{iters} iterations, {el:.1f} s")
     N = X.shape[0]
     return {"value": N * iters / el, "unit": "samples/s", "cores": torch.get_num_threads(), "kind": "port",
             "sample": f"oracle/cp_oracle.py fit_Adam (torch {torch.__version__} CPU, the reference's op order) on "
                       f"the same {N} x {list(cfg['dims'])} X (full per-GPU size), {iters} timed iterations after 2 "
-                      f"warm-up ({el:.1f} s), torch.set_num_threads({nthreads}) = every CPU in this process's "
-                      f"affinity",
+                      f"warm-up ({el:.1f} s), torch.set_num_threads({nthreads}) "
+                      f"({'OMP_NUM_THREADS quota of this job' if threads is None and quota else 'threads'})",
             "host": info, "ms_per_step": 1e3 * el / iters}
 
 

@@ -202,6 +202,28 @@ int tr_adam_step(tr_plan* plan, float* params, const float* grad, float* exp_avg
 int tr_plan_set_prepare_next(tr_plan* plan, int enable);
 
 /*
+ * float64 linear model: CP_linear_regression(..., dtype=torch.float64) (standard…py:206; the
+ * reference's KAT-1, demo_TensorRegression.ipynb, is an fp64 LBFGS fit).  Same arenas and
+ * semantics as the fp32 entry points above with double buffers (X, y, params, weights, grad,
+ * Adam state, outputs); the plan computes in double (two passes over X on the VALU).  A float64
+ * plan accepts only the _f64 entry points, a float32 plan only the float ones (TR_E_ARG).
+ */
+int tr_plan_create_f64(tr_plan** out, int device, int n_feature_modes, const int64_t* feature_dims, int rank,
+                       int64_t max_rows, const int32_t* non_negative, double softplus_beta,
+                       double softplus_threshold);
+int tr_forward_f64(tr_plan* plan, const double* X, int64_t n_rows, const double* params, const double* weights,
+                   double* out, void* stream);
+int tr_loss_grad_f64(tr_plan* plan, const double* X, int64_t n_rows, const double* y, double norm,
+                     const double* params, const double* weights, double* grad_out, double* yhat_out,
+                     const int32_t* stop_flag, void* stream);
+int tr_finalize_grad_f64(tr_plan* plan, const double* params, const double* grad, double lambda_l2,
+                         double* grad_total_out, double* loss_out, void* stream);
+int tr_adam_step_f64(tr_plan* plan, double* params, const double* grad, double* exp_avg, double* exp_avg_sq,
+                     double* max_exp_avg_sq, double lambda_l2, double lr, double beta1, double beta2, double eps,
+                     double weight_decay, int amsgrad, int64_t step, double* loss_hist, int64_t hist_base,
+                     int64_t iter, int64_t patience, double tol, int32_t* stop_flag, void* stream);
+
+/*
  * Spectral model plan (spectral_tensor_regression.CP_linear_regression, spectral…py:424-539;
  * fit model lin_model :118-165 + stepwise_spectral_model :339-390; predict model
  * lin_model + spectral_model :168-220).  X is (N, n_w, n_d) fp32, y is (N, n_out) fp32.

@@ -133,11 +133,19 @@ class Plan:
     """Owns one `tr_plan` (workspace + kernel strategy) for a model shape."""
 
     def __init__(self, model, feature_dims, n_classes, rank, max_rows, non_negative, softplus_kwargs,
-                 device):
+                 device, dtype=torch.float32):
         self.lib = _lib.load()
         self.dev = device_index(device)
         self.device_str = f"cuda:{self.dev}"
         self.model = model
+        if dtype not in (torch.float32, torch.float64):
+            raise NotImplementedError(f"the gfx950 kernels compute in float32 or float64; got dtype={dtype}")
+        if dtype == torch.float64 and model != _lib.TR_MODEL_LINEAR:
+            raise NotImplementedError("float64 is offered for CP_linear_regression only (the reference's multinomial "
+                                      "class is float32-only, multinomial_tensor_regression.py:255)")
+        self.dtype = dtype
+        self.f64 = dtype == torch.float64
+        self._sfx = "_f64" if self.f64 else ""
         self.feature_dims = [int(d) for d in feature_dims]
         self.n_classes = int(n_classes)
         self.rank = int(rank)
@@ -150,9 +158,13 @@ class Plan:
         nna = (ctypes.c_int32 * nf)(*nn)
         h = ctypes.c_void_p()
         with torch.cuda.device(self.dev):
-            rc = self.lib.tr_plan_create(ctypes.byref(h), self.dev, model, len(self.feature_dims), dims,
-                                         self.n_classes, self.rank, max(1, self.max_rows), nna, beta, thr)
-        check(rc, "tr_plan_create")
+            if self.f64:
+                rc = self.lib.tr_plan_create_f64(ctypes.byref(h), self.dev, len(self.feature_dims), dims, self.rank,
+                                                 max(1, self.max_rows), nna, beta, thr)
+            else:
+                rc = self.lib.tr_plan_create(ctypes.byref(h), self.dev, model, len(self.feature_dims), dims,
+                                             self.n_classes, self.rank, max(1, self.max_rows), nna, beta, thr)
+        check(rc, "tr_plan_create" + self._sfx)
         self.h = h
         _track(self)
         self.num_params = int(self.lib.tr_plan_num_params(h))
@@ -183,7 +195,7 @@ class Plan:
         return [(d, self.rank) for d in dims]
 
     def pack(self, Bcp, bias=None):
-        arena = torch.empty(self.num_params, dtype=torch.float32, device=f"cuda:{self.dev}")
+        arena = torch.empty(self.num_params, dtype=self.dtype, device=f"cuda:{self.dev}")
         shapes = self.factor_shapes()
         if len(Bcp) != len(shapes):
             raise ValueError(f"expected {len(shapes)} Kruskal factors, got {len(Bcp)}")
@@ -280,31 +292,38 @@ class Plan:
         C = self.n_classes if self.model == _lib.TR_MODEL_MULTINOMIAL else 1
         if out is None:
             shape = (N, C) if self.model == _lib.TR_MODEL_MULTINOMIAL else (N,)
-            out = torch.empty(shape, dtype=torch.float32, device=X.device)
+            out = torch.empty(shape, dtype=self.dtype, device=X.device)
         self._set_stride(X)
-        rc = self.lib.tr_forward(self.h, ptr(X), N, ptr(arena), ptr(weights), ptr(out), stream_handle(self.dev))
-        check(rc, "tr_forward")
+        fwd = self.lib.tr_forward_f64 if self.f64 else self.lib.tr_forward
+        rc = fwd(self.h, ptr(X), N, ptr(arena), ptr(weights), ptr(out), stream_handle(self.dev))
+        check(rc, "tr_forward" + self._sfx)
         return out
 
     def loss_grad(self, X, target, class_weight, norm, arena, weights, grad, yhat=None, stop=None):
         self._set_stride(X)
-        rc = self.lib.tr_loss_grad(self.h, ptr(X), X.shape[0], ptr(target), ptr(class_weight), float(norm),
-                                   ptr(arena), ptr(weights), ptr(grad), ptr(yhat), ptr(stop),
-                                   stream_handle(self.dev))
-        check(rc, "tr_loss_grad")
+        if self.f64:
+            rc = self.lib.tr_loss_grad_f64(self.h, ptr(X), X.shape[0], ptr(target), float(norm), ptr(arena),
+                                           ptr(weights), ptr(grad), ptr(yhat), ptr(stop), stream_handle(self.dev))
+        else:
+            rc = self.lib.tr_loss_grad(self.h, ptr(X), X.shape[0], ptr(target), ptr(class_weight), float(norm),
+                                       ptr(arena), ptr(weights), ptr(grad), ptr(yhat), ptr(stop),
+                                       stream_handle(self.dev))
+        check(rc, "tr_loss_grad" + self._sfx)
 
     def finalize_grad(self, arena, grad, lambda_l2, grad_total, loss_out):
-        rc = self.lib.tr_finalize_grad(self.h, ptr(arena), ptr(grad), float(lambda_l2), ptr(grad_total),
-                                       ptr(loss_out), stream_handle(self.dev))
-        check(rc, "tr_finalize_grad")
+        fin = self.lib.tr_finalize_grad_f64 if self.f64 else self.lib.tr_finalize_grad
+        rc = fin(self.h, ptr(arena), ptr(grad), float(lambda_l2), ptr(grad_total), ptr(loss_out),
+                 stream_handle(self.dev))
+        check(rc, "tr_finalize_grad" + self._sfx)
 
     def adam_step(self, arena, grad, m, v, vmax, lambda_l2, hp, step, hist, hist_base, it, patience, tol,
                   stop):
-        rc = self.lib.tr_adam_step(self.h, ptr(arena), ptr(grad), ptr(m), ptr(v), ptr(vmax), float(lambda_l2),
-                                   hp["lr"], hp["beta1"], hp["beta2"], hp["eps"], hp["weight_decay"],
-                                   1 if hp["amsgrad"] else 0, int(step), ptr(hist), int(hist_base), int(it),
-                                   int(patience), float(tol), ptr(stop), stream_handle(self.dev))
-        check(rc, "tr_adam_step")
+        step_fn = self.lib.tr_adam_step_f64 if self.f64 else self.lib.tr_adam_step
+        rc = step_fn(self.h, ptr(arena), ptr(grad), ptr(m), ptr(v), ptr(vmax), float(lambda_l2),
+                     hp["lr"], hp["beta1"], hp["beta2"], hp["eps"], hp["weight_decay"],
+                     1 if hp["amsgrad"] else 0, int(step), ptr(hist), int(hist_base), int(it),
+                     int(patience), float(tol), ptr(stop), stream_handle(self.dev))
+        check(rc, "tr_adam_step" + self._sfx)
 
 
 class SpectralPlan(Plan):
@@ -317,6 +336,7 @@ class SpectralPlan(Plan):
         self.dev = device_index(device)
         self.device_str = f"cuda:{self.dev}"
         self.model = _lib.TR_MODEL_SPECTRAL
+        self.dtype, self.f64, self._sfx = torch.float32, False, ""
         self.dims = (int(n_w), int(n_d), int(n_out))
         self.rank_normal, self.rank_spectral, self.n_complex = int(rank_normal), int(rank_spectral), int(n_complex)
         self.max_rows = int(max_rows)
@@ -394,14 +414,14 @@ def _rows_contiguous(X):
     return X.ndim >= 1 and X.stride(0) >= 1
 
 
-def as_device_rows(X, dev):
-    """X as an fp32 tensor on cuda:dev whose samples X[n] are contiguous blocks; the stride along
+def as_device_rows(X, dev, dtype=torch.float32):
+    """X as a `dtype` tensor on cuda:dev whose samples X[n] are contiguous blocks; the stride along
     dim 0 is kept (strided / windowed views, e.g. util.windowed_view, are NOT materialised).  A
     view the 16-byte kernel paths cannot read (misaligned base with a stride % 4 == 0) is copied."""
     if not isinstance(X, torch.Tensor):
-        X = torch.as_tensor(np.asarray(X), dtype=torch.float32)
-    if X.dtype != torch.float32:
-        raise TypeError(f"the gfx950 path computes in fp32; got X of dtype {X.dtype}")
+        X = torch.as_tensor(np.asarray(X), dtype=dtype)
+    if X.dtype != dtype:
+        raise TypeError(f"the gfx950 path of this model computes in {dtype}; got X of dtype {X.dtype}")
     if X.device.type != "cuda" or X.device.index != dev:
         X = X.to(f"cuda:{dev}")
     if not _rows_contiguous(X) or (X.stride(0) % 4 == 0 and X.data_ptr() % 16 != 0):
@@ -409,12 +429,12 @@ def as_device_rows(X, dev):
     return X
 
 
-def as_device_f32(X, dev):
-    """X as a contiguous fp32 tensor on cuda:dev (copies only when needed)."""
+def as_device_f32(X, dev, dtype=torch.float32):
+    """X as a contiguous `dtype` tensor on cuda:dev (copies only when needed)."""
     if not isinstance(X, torch.Tensor):
-        X = torch.as_tensor(np.asarray(X), dtype=torch.float32)
-    if X.dtype != torch.float32:
-        raise TypeError(f"the gfx950 path computes in fp32; got X of dtype {X.dtype}")
+        X = torch.as_tensor(np.asarray(X), dtype=dtype)
+    if X.dtype != dtype:
+        raise TypeError(f"the gfx950 path of this model computes in {dtype}; got a tensor of dtype {X.dtype}")
     if X.device.type != "cuda" or X.device.index != dev:
         X = X.to(f"cuda:{dev}")
     return X.contiguous()
@@ -474,6 +494,7 @@ def run_adam_fit(plan, X, target, class_weight, norm, arena, weights, lambda_L2,
     data loss and the device status slot — runs between the local gradient and the Adam step.
     """
     dev = plan.device_str
+    fdt = getattr(plan, "dtype", torch.float32)
     allreduce = None
     if process_group is not None:
         import torch.distributed as dist
@@ -481,7 +502,7 @@ def run_adam_fit(plan, X, target, class_weight, norm, arena, weights, lambda_L2,
 
         def allreduce(g):
             dist.all_reduce(g, group=process_group)
-    opts = dict(dtype=torch.float32, device=dev)
+    opts = dict(dtype=fdt, device=dev)
     grad = torch.zeros(plan.num_grads, **opts)
     m = torch.zeros(plan.num_params, **opts)
     v = torch.zeros(plan.num_params, **opts)

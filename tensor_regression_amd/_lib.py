@@ -53,6 +53,14 @@ SIGNATURES = {
                                 _c.c_double, _c.c_double, _c.c_double, _c.c_int, _c.c_int64, _vp,
                                 _c.c_int64, _c.c_int64, _c.c_int64, _c.c_double, _vp, _vp]),
     "tr_plan_set_prepare_next": (_c.c_int, [_vp, _c.c_int]),
+    "tr_plan_create_f64": (_c.c_int, [_c.POINTER(_vp), _c.c_int, _c.c_int, _c.POINTER(_c.c_int64), _c.c_int,
+                                      _c.c_int64, _c.POINTER(_c.c_int32), _c.c_double, _c.c_double]),
+    "tr_forward_f64": (_c.c_int, [_vp, _vp, _c.c_int64, _vp, _vp, _vp, _vp]),
+    "tr_loss_grad_f64": (_c.c_int, [_vp, _vp, _c.c_int64, _vp, _c.c_double, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "tr_finalize_grad_f64": (_c.c_int, [_vp, _vp, _vp, _c.c_double, _vp, _vp, _vp]),
+    "tr_adam_step_f64": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _c.c_double, _c.c_double, _c.c_double,
+                                    _c.c_double, _c.c_double, _c.c_double, _c.c_int, _c.c_int64, _vp,
+                                    _c.c_int64, _c.c_int64, _c.c_int64, _c.c_double, _vp, _vp]),
 }
 
 _lock = threading.Lock()

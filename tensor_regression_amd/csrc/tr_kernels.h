@@ -107,6 +107,9 @@ hipError_t launch_update(const FactorSet& fs, int n_bias, float* params, const f
                          const UpdateArgs& ua, float* m, float* v, float* vmax, float* grad_total_out,
                          float* loss_out, double* loss_hist, int32_t* stop, hipStream_t st,
                          const PrepArgs* prep = nullptr);
+// the plateau test alone (fit_Adam's stop rule, standard…py:467-470) on the fp64 loss history
+hipError_t launch_converge(const double* loss_hist, int64_t hist_base, int64_t iter, int64_t patience, double tol,
+                           int32_t* stop, hipStream_t st);
 // whether k_update can prepare the next iteration in this mode for this factor set
 bool update_prepare_mode_ok(const FactorSet& fs, int mode);
 

@@ -1450,6 +1450,12 @@ hipError_t launch_cols_wide(int C, int W, int64_t nstripes, int64_t nchunks, con
   return hipSuccess;
 }
 
+hipError_t launch_converge(const double* loss_hist, int64_t hist_base, int64_t iter, int64_t patience, double tol,
+                           int32_t* stop, hipStream_t st) {
+  hipLaunchKernelGGL(k_converge, dim3(1), dim3(64), 0, st, loss_hist, hist_base, iter, patience, tol, stop);
+  return hipGetLastError();
+}
+
 // ---- slab reduction --------------------------------------------------------------------------
 hipError_t launch_reduce_slabs(int W, const float* part, int64_t nslabs, int64_t ncols, float* out,
                                const double* dpart, int64_t nd, double loss_scale, float* loss_slot,

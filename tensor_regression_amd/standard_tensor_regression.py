@@ -9,7 +9,8 @@ the hot path — softplus + cp_to_tensor + inner(X, B) + MSELoss + backward + Ad
 no torch.autograd on that path.
 
 Differences from the reference (all deliberate):
-  * tensors must live on a HIP device (`device='cuda'`); fp32 only on the kernel path;
+  * tensors must live on a HIP device (`device='cuda'`); the kernels compute in the model's
+    dtype, float32 or float64 (dtype=torch.float64: a float64 two-pass path, csrc/tr_fp64.hip);
   * `lin_model` returns a non-differentiable tensor (the fit loops compute gradients in HIP);
   * a 2-D `y` is rejected (the reference silently broadcasts (N,) - (N,1) to (N,N), quirk Q11);
   * `fit_Adam` takes an optional `process_group` to fit sample shards over torch.distributed.
@@ -58,14 +59,15 @@ def non_neg_fn(B_cp, non_negative, softplus_kwargs=None):
 _plan_cache = {}
 
 
-def _plan_for(model, feature_dims, n_classes, rank, rows, non_negative, softplus_kwargs, device):
+def _plan_for(model, feature_dims, n_classes, rank, rows, non_negative, softplus_kwargs, device,
+              dtype=torch.float32):
     nf = len(feature_dims) + (1 if model == _lib.TR_MODEL_MULTINOMIAL else 0)
     beta, thr = _engine.softplus_params(softplus_kwargs)
     key = (model, tuple(int(d) for d in feature_dims), int(n_classes), int(rank),
-           tuple(bool(non_negative[f]) for f in range(nf)), beta, thr, _engine.device_index(device))
+           tuple(bool(non_negative[f]) for f in range(nf)), beta, thr, _engine.device_index(device), dtype)
     p = _plan_cache.get(key)
     if p is None or p.max_rows < rows:
-        p = Plan(model, feature_dims, n_classes, rank, rows, non_negative, softplus_kwargs, device)
+        p = Plan(model, feature_dims, n_classes, rank, rows, non_negative, softplus_kwargs, device, dtype=dtype)
         _plan_cache[key] = p
     return p
 
@@ -84,10 +86,15 @@ def lin_model(X, Bcp, weights, non_negative, bias, softplus_kwargs=None):
                          f"tensor_1.shape={list(X.shape)}, factors={[tuple(A.shape) for A in Bcp]}")
     rank = int(Bcp[0].shape[1])
     dev = X.device
-    Xd = _engine.as_device_rows(X, dev.index)
-    plan = _plan_for(_lib.TR_MODEL_LINEAR, X.shape[1:], 1, rank, 1, non_negative, softplus_kwargs, dev)
+    dtype = X.dtype
+    for A in Bcp:  # inner(X, B) is one matmul in the reference: operands of one dtype
+        if torch.as_tensor(A).dtype != dtype:
+            raise RuntimeError(f"expected m1 and m2 to have the same dtype, but got: {dtype} != "
+                               f"{torch.as_tensor(A).dtype}")
+    Xd = _engine.as_device_rows(X, dev.index, dtype)
+    plan = _plan_for(_lib.TR_MODEL_LINEAR, X.shape[1:], 1, rank, 1, non_negative, softplus_kwargs, dev, dtype)
     arena = plan.pack([torch.as_tensor(A).to(dev) for A in Bcp], torch.as_tensor(bias).to(dev))
-    w = torch.as_tensor(weights, dtype=torch.float32).to(dev).contiguous()
+    w = torch.as_tensor(weights, dtype=dtype).to(dev).contiguous()
     return plan.forward(Xd, arena, w)
 
 
@@ -172,10 +179,10 @@ class CP_linear_regression():
         self._plan = None
 
     # ---- plumbing --------------------------------------------------------------------------
-    def _check_fp32(self):
-        if self.dtype != torch.float32:
-            raise NotImplementedError(f"the gfx950 kernels compute in fp32; this model was built with "
-                                      f"dtype={self.dtype}")
+    def _check_dtype(self):
+        if self.dtype not in (torch.float32, torch.float64):
+            raise NotImplementedError(f"the gfx950 kernels compute in float32 or float64; this model was built "
+                                      f"with dtype={self.dtype}")
 
     def _get_plan(self, X, rows):
         from .util import HostStream
@@ -188,28 +195,31 @@ class CP_linear_regression():
         p = self._plan
         dev = _engine.device_index(X.device if isinstance(X, torch.Tensor) else f"cuda:{X.dev_index}")
         if (p is None or p.max_rows < rows or p.feature_dims != dims or p.rank != int(self.Bcp[0].shape[1])
-                or p.dev != dev or p.nonlin != _engine.nonlin_key(self.non_negative, self.softplus_kwargs, len(dims))):
+                or p.dev != dev or p.dtype != self.dtype
+                or p.nonlin != _engine.nonlin_key(self.non_negative, self.softplus_kwargs, len(dims))):
             p = Plan(_lib.TR_MODEL_LINEAR, dims, 1, int(self.Bcp[0].shape[1]), rows, self.non_negative,
-                     self.softplus_kwargs, f"cuda:{dev}")
+                     self.softplus_kwargs, f"cuda:{dev}", dtype=self.dtype)
             self._plan = p
         return p
 
     def _inputs(self, X, y):
-        self._check_fp32()
+        self._check_dtype()
         from .util import HostStream
         if isinstance(X, HostStream):  # out-of-core: X streams from host memory every iteration
+            if self.dtype != torch.float32:
+                raise NotImplementedError("HostStream streams float32 samples; this model is float64")
             dev = X.dev_index
             y = torch.as_tensor(y)
             if y.ndim != 1 or y.shape[0] != len(X):
                 raise ValueError(f"y must be 1-D with len(y) == len(X); got y.shape={tuple(y.shape)}")
             return X, as_device_f32(y, dev), dev
         dev = _engine.compute_device(X, self.device)
-        X = _engine.as_device_rows(X, dev)
+        X = _engine.as_device_rows(X, dev, self.dtype)
         y = torch.as_tensor(y)
         if y.ndim != 1 or y.shape[0] != X.shape[0]:
             raise ValueError(f"y must be 1-D with len(y) == X.shape[0]; got y.shape={tuple(y.shape)}, "
                              f"X.shape[0]={X.shape[0]}")
-        y = as_device_f32(y, dev)
+        y = as_device_f32(y, dev, self.dtype)
         return X, y, dev
 
     # ---- fitting -----------------------------------------------------------------------------
@@ -227,8 +237,8 @@ class CP_linear_regression():
         plan = self._get_plan(X, N)
         params = self.Bcp + [self.bias]
         optimizer = torch.optim.LBFGS(params, **LBFGS_kwargs)
-        w = self.weights.to(f"cuda:{dev}", torch.float32).contiguous()
-        opts = dict(dtype=torch.float32, device=f"cuda:{dev}")
+        w = self.weights.to(f"cuda:{dev}", self.dtype).contiguous()
+        opts = dict(dtype=self.dtype, device=f"cuda:{dev}")
         grad = torch.zeros(plan.num_grads, **opts)
         gtot = torch.zeros(plan.num_params, **opts)
         loss_out = torch.zeros(1, **opts)
@@ -286,7 +296,7 @@ class CP_linear_regression():
             dist.all_reduce(n_t, group=process_group)
             n_global = float(n_t.item())
         arena = plan.pack(self.Bcp, self.bias)
-        w = self.weights.to(f"cuda:{dev}", torch.float32).contiguous()
+        w = self.weights.to(f"cuda:{dev}", self.dtype).contiguous()
         vcb = _VerbosePrinter(plan, X, y, w) if verbose == 2 else None
         convergence_reached, _ = run_adam_fit(plan, X, y, None, n_global, arena, w, lambda_L2, max_iter, tol,
                                               patience, hp, self.loss_running, verbose_cb=vcb,

@@ -16,29 +16,31 @@ def names(prefix=""):
     return out
 
 
-def split(flat, shapes):
+def split(flat, shapes, dtype=np.float32):
     out, k = [], 0
     for s in shapes:
         n = int(np.prod(s))
-        out.append(np.asarray(flat[k:k + n], dtype=np.float32).reshape(s))
+        out.append(np.asarray(flat[k:k + n], dtype=dtype).reshape(s))
         k += n
     return out
 
 
 def load(name):
+    """A fixture with its factor lists split; float64 fixtures (f64_*) keep float64 inputs."""
     d = dict(np.load(os.path.join(GOLDEN, name + ".npz")))
     meta = json.loads(str(d.pop("meta")))
     shapes = [tuple(s) for s in meta["factor_shapes"]]
-    d["X"] = torch.tensor(d["X_q"].astype(np.float32) / 8.0)
-    d["Bcp0_list"] = split(d["Bcp0"], shapes)
+    dt = np.float64 if meta.get("model") == "linear_f64" else np.float32
+    d["X"] = torch.tensor(d["X_q"].astype(dt) / 8.0)
+    d["Bcp0_list"] = split(d["Bcp0"], shapes, dt)
     if "Bcp_final" in d:
-        d["Bcp_final_list"] = split(d["Bcp_final"], shapes)
+        d["Bcp_final_list"] = split(d["Bcp_final"], shapes, dt)
     if "grads0" in d:
-        d["grads0_list"] = split(d["grads0"], shapes)
+        d["grads0_list"] = split(d["grads0"], shapes, dt)
     if "Bcp_10" in d:
-        d["Bcp_10_list"] = split(d["Bcp_10"], shapes)
+        d["Bcp_10_list"] = split(d["Bcp_10"], shapes, dt)
     if "Bcp_final2" in d:
-        d["Bcp_final2_list"] = split(d["Bcp_final2"], shapes)
+        d["Bcp_final2_list"] = split(d["Bcp_final2"], shapes, dt)
     d["meta"] = meta
     d["shapes"] = shapes
     return d

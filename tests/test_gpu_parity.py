@@ -640,3 +640,83 @@ def test_cluster_device_failure(monkeypatch, policy):
     assert len(m.loss_running) == 12 and np.all(np.isfinite(m.loss_running))
     np.testing.assert_allclose(m.loss_running, ref.loss_running, rtol=RTOL)
     _assert_factors(m.Bcp, [a.detach().cpu().numpy() for a in ref.Bcp])
+
+
+# ------------------------------------------------------------------------------------------------
+# float64 linear model: CP_linear_regression(dtype=torch.float64) (standard…py:206), csrc/tr_fp64.hip
+# ------------------------------------------------------------------------------------------------
+F64_RTOL = 1e-10  # fp64: reduction-order differences are ~1e-15 per pass
+
+
+@pytest.mark.parametrize("name", names("f64_"))
+def test_float64_golden(name):
+    """One loss + gradient at the reference's initial point and the whole Adam / LBFGS trajectory
+    of the reference's fp64 fit, through the _f64 C entry points."""
+    from tensor_regression_amd import CP_linear_regression
+    from tensor_regression_amd.standard_tensor_regression import lin_model
+    d = load(name)
+    m = d["meta"]
+    X = d["X"].to(DEV)
+    y = torch.tensor(d["y"], device=DEV)
+    assert X.dtype == y.dtype == torch.float64
+
+    def make():
+        Bcp = [torch.tensor(a, device=DEV).requires_grad_(True) for a in d["Bcp0_list"]]
+        return CP_linear_regression(X.shape, dtype=torch.float64, rank=m["rank"], non_negative=m["non_negative"],
+                                    Bcp_init=Bcp, bias_init=float(d["bias0"][0]), device=DEV)
+
+    model = make()
+    yh = lin_model(X, model.Bcp, model.weights, model.non_negative, model.bias, model.softplus_kwargs)
+    assert yh.dtype == torch.float64
+    np.testing.assert_allclose(yh.cpu().numpy(), d["y_hat0"], rtol=F64_RTOL, atol=F64_RTOL * np.abs(d["y_hat0"]).max())
+    plan = model._get_plan(X, X.shape[0])
+    assert "float64" in plan.describe
+    arena = plan.pack(model.Bcp, model.bias)
+    grad = torch.zeros(plan.num_grads, dtype=torch.float64, device=DEV)
+    gtot = torch.zeros(plan.num_params, dtype=torch.float64, device=DEV)
+    loss = torch.zeros(1, dtype=torch.float64, device=DEV)
+    plan.loss_grad(X, y, None, float(X.shape[0]), arena, model.weights, grad)
+    plan.finalize_grad(arena, grad, m["lambda_L2"], gtot, loss)
+    assert abs(loss.item() - d["loss0"]) <= F64_RTOL * abs(d["loss0"])
+    _assert_factors(plan.factor_views(gtot), d["grads0_list"], tol=F64_RTOL)
+    assert abs(gtot[-1].item() - float(d["bias_grad0"][0])) <= F64_RTOL * max(1.0, abs(float(d["bias_grad0"][0])))
+    model = make()
+    if m["lbfgs_kwargs"] is not None:
+        conv = model.fit(X, y, lambda_L2=m["lambda_L2"], max_iter=m["max_iter"], tol=0.0, patience=100,
+                         running_loss_logging_interval=m["logging_interval"], LBFGS_kwargs=m["lbfgs_kwargs"])
+        tol = 1e-8  # strong-Wolfe line searches amplify the 1e-15 differences step by step
+    else:
+        conv = model.fit_Adam(X, y, lambda_L2=m["lambda_L2"], max_iter=m["max_iter"], tol=0.0, patience=10,
+                              Adam_kwargs=m["adam_kwargs"])
+        tol = F64_RTOL
+    assert int(conv) == int(d["converged"])
+    assert len(model.loss_running) == len(d["loss_running"])
+    np.testing.assert_allclose(model.loss_running, d["loss_running"], rtol=tol)
+    _assert_factors(model.Bcp, d["Bcp_final_list"], tol=100 * tol)
+    assert model.Bcp[0].dtype == torch.float64
+
+
+@pytest.mark.slow
+def test_kat1_notebook_trace_on_gpu():
+    """KAT-1 (demo_TensorRegression.ipynb): CP_linear_regression in float64 on X (2000, 500, 500),
+    rank 10, LBFGS strong-Wolfe, lambda 1e-5, run to the plateau stop.  The reference itself
+    replays the notebook's printed trace to 9.3e-5 (tests/golden/kat_replay.json, its own fp64
+    run here: 13 logged losses); the GPU float64 fit must follow that replay to 1e-6 and stop at
+    the same length."""
+    import json
+    from kat_data import KAT1_TRACE, kat_inputs
+    from tensor_regression_amd import CP_linear_regression
+    from golden_util import GOLDEN
+    rep = json.load(open(GOLDEN + "/kat_replay.json"))
+    X, y = kat_inputs("kat1")
+    m = CP_linear_regression(X.shape, dtype=X.dtype, rank=10, non_negative=[False, False], Bcp_init_scale=0.005,
+                             softplus_kwargs={'beta': 50, 'threshold': 1}, device=DEV)
+    Xd, yd = X.to(DEV), y.to(DEV)
+    del X
+    m.fit(Xd, yd, lambda_L2=1e-5, max_iter=200, tol=1e-50, patience=10, running_loss_logging_interval=1,
+          LBFGS_kwargs={'lr': 1, 'max_iter': 20, 'max_eval': None, 'tolerance_grad': 1e-07, 'tolerance_change': 1e-09,
+                        'history_size': 100, 'line_search_fn': "strong_wolfe"})
+    assert len(m.loss_running) == rep["kat1_len"]
+    np.testing.assert_allclose(m.loss_running, rep["kat1_loss_running"], rtol=1e-6)
+    n = min(len(m.loss_running), len(KAT1_TRACE))
+    assert np.max(np.abs(np.array(m.loss_running[:n]) - KAT1_TRACE[:n]) / np.abs(KAT1_TRACE[:n])) <= 2 * rep["kat1_max_rel"]

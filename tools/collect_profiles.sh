@@ -18,10 +18,11 @@ for c in "$@"; do
     { head -1 $f; grep 'tr::' $f || true; } > profiles/${round}_${c}_pmc_${p}.csv
   done
 done
-python - "$src/traffic.json" <<'PY'
+python - "$src/traffic.json" "$round" <<'PY'
 import json, sys
 new = json.load(open(sys.argv[1]))
 old = json.load(open("profiles/traffic.json"))
 old.update(new)
+old["round"] = f"profile set {sys.argv[2]}"
 json.dump(old, open("profiles/traffic.json", "w"), indent=1)
 PY

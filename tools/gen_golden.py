@@ -165,6 +165,45 @@ def mnl_case(name, seed, shape, n_classes, rank, non_negative, class_w, lam, ada
          loss_running_10=np.array(m10.loss_running), meta=np.array(json.dumps(meta)))
 
 
+def f64_case(name, seed, shape, rank, lam, iters, adam_kwargs=None, lbfgs_kwargs=None, non_negative=None,
+             logging_interval=1):
+    """CP_linear_regression(dtype=torch.float64) (standard…py:206): fit_Adam or fit (LBFGS) in
+    float64 through the reference, plus one loss + gradient at the initial point."""
+    rng = np.random.default_rng(seed)
+    Xq, X32 = exact_X(rng, shape)
+    X = X32.double()
+    y = torch.tensor(rng.standard_normal(shape[0]))
+    nn = non_negative if non_negative is not None else [False] * len(shape)
+    torch.manual_seed(seed)
+    m = STR.CP_linear_regression(X.shape, dtype=torch.float64, rank=rank, non_negative=nn, bias_init=0.1)
+    Bcp0 = [A.detach().numpy().copy() for A in m.Bcp]
+    b0 = m.bias.detach().numpy().copy()
+    y_hat = STR.lin_model(X, m.Bcp, m.weights, m.non_negative, m.bias, softplus_kwargs=m.softplus_kwargs)
+    loss = torch.nn.MSELoss()(y_hat, y) + lam * STR.L2_penalty(m.Bcp)
+    loss.backward()
+    grads = [A.grad.numpy().copy() for A in m.Bcp]
+    bgrad = m.bias.grad.numpy().copy()
+    for A in m.Bcp:
+        A.grad = None
+    m.bias.grad = None
+    if lbfgs_kwargs is not None:
+        conv = m.fit(X, y, lambda_L2=lam, max_iter=iters, tol=0.0, patience=100, verbose=False,
+                     running_loss_logging_interval=logging_interval, LBFGS_kwargs=dict(lbfgs_kwargs))
+    else:
+        conv = m.fit_Adam(X, y, lambda_L2=lam, max_iter=iters, tol=0.0, patience=10, verbose=False,
+                          Adam_kwargs=dict(adam_kwargs))
+    meta = dict(model="linear_f64", seed=seed, shape=list(shape), rank=rank, non_negative=list(map(bool, nn)),
+                lambda_L2=lam, max_iter=iters, adam_kwargs=adam_kwargs, lbfgs_kwargs=lbfgs_kwargs,
+                logging_interval=logging_interval, softplus_kwargs=m.softplus_kwargs,
+                factor_shapes=[list(a.shape) for a in Bcp0], torch=torch.__version__)
+    save(name, X_q=Xq, y=y.numpy(), Bcp0=np.concatenate([a.reshape(-1) for a in Bcp0]), bias0=b0,
+         y_hat0=y_hat.detach().numpy(), loss0=np.float64(loss.item()),
+         grads0=np.concatenate([g.reshape(-1) for g in grads]), bias_grad0=bgrad,
+         loss_running=np.array(m.loss_running, dtype=np.float64),
+         Bcp_final=np.concatenate([A.detach().numpy().reshape(-1) for A in m.Bcp]),
+         bias_final=m.bias.detach().numpy().copy(), converged=np.int32(conv), meta=np.array(json.dumps(meta)))
+
+
 def mnl_lbfgs_case(name, seed, shape, n_classes, rank, class_w, lam, iters, lbfgs_kwargs, logging_interval=1):
     """CP_logistic_regression.fit (LBFGS, multinomial…py:291-387): logged loss = data CE only (:372)."""
     rng = np.random.default_rng(seed)
@@ -410,6 +449,11 @@ def main():
     mnl_lbfgs_case("mnllbfgs_weighted", 26, (96, 6, 5), 4, 3, [0.5, 2.0, 1.0, 1.5], 1e-2, 8,
                    {'lr': 0.05, 'max_iter': 3, 'max_eval': None, 'tolerance_grad': 1e-07,
                     'tolerance_change': 1e-09, 'history_size': 10, 'line_search_fn': None}, logging_interval=2)
+    f64_case("f64_adam", 61, (200, 12, 9), 3, 0.01, 60, adam_kwargs={'lr': 0.02, 'amsgrad': True},
+             non_negative=[True, False, False])
+    f64_case("f64_lbfgs", 62, (150, 10, 8), 2, 1e-3, 8,
+             lbfgs_kwargs={'lr': 1, 'max_iter': 20, 'max_eval': None, 'tolerance_grad': 1e-07,
+                           'tolerance_change': 1e-09, 'history_size': 100, 'line_search_fn': "strong_wolfe"})
     windowed_case("win_lin", 51, (300, 12), (-4, 4), 3, 0.01, adam, 50)
     windowed_case("win_lin_asym", 52, (200, 6, 5), (0, 5), 2, 0.01, {'lr': 0.02, 'amsgrad': True}, 30)
     windowed_case("win_mnl", 53, (260, 10), (-3, 5), 2, 0.01, adam, 40, n_classes=3)
