@@ -33,21 +33,22 @@ METRIC = "training samples/sec + achieved HBM GB/s, 3-D CP regression rank=8, 1/
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 CONFIGS = {
-    "c2": dict(kind="linear", rows=65536, dims=(256, 128), rank=8,
+    "c2": dict(kind="linear", rows=65536, dims=(256, 128), rank=8, expect="fused-1pass",
                workload="configs[1]: 3-D standard CP regression, X (65536, 256, 128) fp32 per GPU, rank 8, "
                         "MSE + L2 (lambda 0.01), Adam lr 0.01"),
-    "c3": dict(kind="multinomial", rows=65536, dims=(128, 64), rank=8, classes=10,
+    "c3": dict(kind="multinomial", rows=65536, dims=(128, 64), rank=8, classes=10, expect="mnl-fused-1pass",
                workload="configs[2]: multinomial CP regression, X (65536, 128, 64) fp32 per GPU, 10 classes, "
                         "rank 8, softmax + weighted CE + L2, Adam lr 0.01"),
-    "c4": dict(kind="linear", rows=16384, dims=(64, 64, 32), rank=16,
+    "c4": dict(kind="linear", rows=16384, dims=(64, 64, 32), rank=16, expect="cluster-1pass",
                workload="configs[3]: 4-D CP regression, X (131072, 64, 64, 32) sharded 16384 samples per GPU, "
                         "rank 16, Adam lr 0.01"),
     "c5": dict(kind="spectral", rows=32768, dims=(256, 129), rank=8, rank_spectral=8, n_complex_dim=1, n_out=2,
+               expect="fused-1pass-mfma",
                workload="configs[4]: spectral_tensor_regression.py fit_Adam, X (32768, 256, 129) fp32 (real: the "
                         "reference rejects complex X; |rfft|-like non-negative synthetic data), rank_normal = "
                         "rank_spectral = 8, n_complex_dim 1, y (32768, 2), Adam lr 0.01"),
 }
-CONFIGS["c6"] = dict(kind="linear", rows=65536, dims=(256, 128), rank=8, windowed=True,
+CONFIGS["c6"] = dict(kind="linear", rows=65536, dims=(256, 128), rank=8, windowed=True, expect="fused-1pass",
                      workload="windowed variant of configs[1] (util.py:67-114 WindowedDataset): 65536 windows of "
                               "256 x 128 over an untiled (65791, 128) fp32 series, read in place through the row "
                               "stride (no materialised windows), rank 8, Adam lr 0.01")
@@ -181,6 +182,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--allow-other-path", action="store_true",
+                    help="measure even when the plan did not take the config's expected kernel path")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--cpu-threads", type=int, default=None, help="CPU baseline threads (default: affinity size)")
     ap.add_argument("--time-all-kernels", action="store_true",
@@ -236,6 +239,12 @@ def main():
 
     fit(args.warmup)
     plan = model._plan
+    # the kernel strategy this config is benchmarked on: a silent fallback (e.g. a spilling
+    # single-pass variant dropping the plan to two passes) must not pass as this config's number
+    want = cfg.get("expect")
+    if want and (f"path={want}" not in plan.describe or "recovered=" in plan.describe) and not args.allow_other_path:
+        raise SystemExit(f"bench {args.config}: plan took an unexpected path ({plan.describe}); expected "
+                         f"path={want} (--allow-other-path to measure it anyway)")
     plan.read_timing()
     # time only the X-streaming kernels by default (2 events per stream launch): timing every
     # tail launch adds event packets between kernels and inflates ms_per_step
