@@ -40,6 +40,10 @@ struct SpecGeom {
   // generic path (tr_spectral_gen.hip) for shapes outside the fused kernel's envelope
   int gen;  // 1: T_n staged through HBM by k_specg_fwd / k_specg_epi / k_specg_bwd
   int gKP;  // K padded to 16 (row stride of the T / dT staging buffer)
+  // column-slice training kernel (tr_spectral_slice.hip) for the shapes it covers (config 5)
+  int sl;                       // 1: SPEC_TRAIN runs k_spec_slice
+  int slDt, sl_Dp;              // rows d >= 128 (<= 2), rows of the phi(A1) / phi(C1) tables
+  int sl_oTail, sl_oEx, sl_oTP, sl_oPart, sl_oN1, sl_oLoss, sl_lds_floats;  // LDS carve (floats)
 };
 
 // Fills g; returns false (with a reason) when the shape is outside the kernels' envelope.
@@ -71,6 +75,14 @@ hipError_t launch_specg(int mode, const SpecGeom& g, int nchunks, const float* X
                         const float* phi, const float* Phi0, const float* wts, const float* y, float scale,
                         float* T, float* slab, int64_t slab_stride, double* dpart, float* out,
                         const int32_t* stop, hipStream_t st);
+// column-slice kernel: eligibility + LDS carve (sets g->sl), occupancy check (may clear g->sl),
+// launch (SPEC_TRAIN only; same outputs as launch_spec_fused)
+void spec_slice_geom(SpecGeom* g);
+hipError_t spec_slice_prepare(SpecGeom* g);
+hipError_t launch_spec_slice(const SpecGeom& g, int grid, const float* X, int64_t N, int64_t xld, const float* phi,
+                             const float* Phi0, const float* wts, const float* y, float scale, float* slab,
+                             int64_t slab_stride, double* dpart, float* out, int64_t rows_per_wg, int reverse,
+                             const int32_t* stop, hipStream_t st);
 // grad[e] = G[e] * dphi[e]  (softplus chain of the reduced phi-space gradient)
 hipError_t launch_spec_chain(int64_t n, const float* G, const float* dphi, float* grad, const int32_t* stop,
                              hipStream_t st);

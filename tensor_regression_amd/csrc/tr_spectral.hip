@@ -860,6 +860,7 @@ bool spec_geom_init(SpecGeom* g, int64_t W, int64_t D, int64_t NO, int Rn, int R
   if (fused_ok && (int64_t)g->lds_floats * 4 > 160 * 1024) fused_ok = false;
   g->gKP = 16 * cdiv_i(K, 16);
   g->gen = fused_ok ? 0 : 1;
+  spec_slice_geom(g);  // the column-slice training kernel where it covers the shape
   if (g->gen) {
     g->KT = g->gKP / 16;
     if (specg_epi_lds_bytes(*g) > 160 * 1024 - 256) {  // (+ the kernel's static loss scratch)

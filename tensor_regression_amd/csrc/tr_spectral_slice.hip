@@ -1,0 +1,665 @@
+// tr_spectral_slice.hip — column-slice single-pass kernel of the spectral fit model
+// (spectral_tensor_regression.py stepwise_spectral_model :339-390 + lin_model :118-165, the
+// fit_Adam loss at :716-717; SURVEY.md §8 row a14, BASELINE config 5).
+//
+// Same math as k_spec_fused (tr_spectral.hip header), different ownership.  k_spec_fused holds
+// one whole sample in LDS and all eight waves walk it in lock-step: forward GEMM, a long
+// epilogue through LDS, gradient GEMM, with block barriers for the LDS-DMA refill; the matrix
+// cores idle through the epilogue and the barriers (39 % busy at config 5).  Here every wave
+// OWNS a private column slice of every sample:
+//
+//   wave wv = (pair p = wv & 3, half hw = wv >> 2) owns d in [32p, 32p+32) (two 16-row d tiles,
+//   interleaved: tile h holds the d with d % 2 == h) and w in [hw*W/2, (hw+1)*W/2).
+//
+//   forward   T_p,hw (32 d x 32 k) = X[w in half, d in pair]^T . Phi0[w in half, :] on
+//             v_mfma_f32_16x16x4_f32, Phi0's B fragments of the half resident in registers;
+//             column tile 0 = the spectral columns (C0, Rs*Cc <= 16), tile 1 = the lin columns
+//             (A0, Rn <= 16)
+//   exchange  the spectral tiles of the two halves are summed (one LDS exchange with the
+//             partner wave wv ^ 4); the lin part is linear in T and needs no exchange
+//   epilogue  Z / V column partials from registers -> one LDS reduction over the 8 waves ->
+//             y_hat, residual, dZ, dV -> dT_n in registers, directly in the MFMA accumulator
+//             layout the gradient GEMM consumes as its B operand (k step i of lane group g
+//             <-> d row 4g + i of the tile)
+//   gradient dPhi0[w in half, :] += X[w in half, d in pair] . dT_n[d in pair, :] into
+//             accumulators that live for the whole launch (summed over the four pairs once,
+//             at the end)
+//
+// so a wave reads only its own slice: it fills the slice by its own LDS-DMA (4-B pieces, any
+// permutation of the 64 floats of a piece) and waits on its own vmcnt — no barrier for X.  The
+// next sample's slice streams into the rows the gradient GEMM has finished with.  Two barriers
+// per sample remain (the partner exchange and the 8-wave column reduction).  Rows d >= 128
+// (D = 129 at config 5) are a VALU forward partial plus one zero-padded k step of the gradient
+// GEMM.  LDS image of a slice: 64 chunks of 2 rows x 32 columns (256 B = one bank row); the
+// 16-B slot of (row, 4-column quad cq) in chunk r is (cq + 8 (row & 1)) ^ swz(r & 7): the forward
+// ds_read_b64 (two d tiles) and the gradient ds_read_b128 (8 consecutive d) are conflict-free.
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+#include <cstring>
+
+#include "tr_common.h"
+#include "tr_spectral.h"
+
+#ifndef TR_SLICE_SKIP
+#define TR_SLICE_SKIP 0  // timing ablation only (results invalid): 1 no LDS-DMA after the first sample,
+                         // 2 no forward MFMAs, 4 no gradient MFMAs
+#endif
+#ifndef TR_SLICE_PROFILE
+#define TR_SLICE_PROFILE 0  // profiling build: per-phase cycle counts of wave 0 of workgroups 0..255
+#endif
+
+namespace tr {
+
+#if TR_SLICE_PROFILE
+__device__ unsigned long long g_slice_prof[256][8][8];  // [workgroup][wave][phase]
+#define SL_MARK(ph)                                                  \
+  do {                                                               \
+    const unsigned long long _now = __builtin_readcyclecounter();    \
+    prof[ph] += _now - prof_t;                                       \
+    prof_t = _now;                                                   \
+  } while (0)
+#define SL_SUB_BEGIN() const unsigned long long _w0 = __builtin_readcyclecounter()
+#define SL_SUB_END(ph) prof[ph] += __builtin_readcyclecounter() - _w0
+#else
+#define SL_MARK(ph) \
+  do {              \
+  } while (0)
+#define SL_SUB_BEGIN() \
+  do {                 \
+  } while (0)
+#define SL_SUB_END(ph) \
+  do {                 \
+  } while (0)
+#endif
+
+namespace {
+typedef float sl_f4 __attribute__((ext_vector_type(4)));
+typedef float sl_f2 __attribute__((ext_vector_type(2)));
+constexpr int SL_NW = 8;
+constexpr int SL_T = SL_NW * TR_WAVE;
+constexpr int SL_ROWS = 128;            // max w rows per wave (W / 2)
+constexpr int SL_SLICE = SL_ROWS * 32;  // floats of one wave's slice
+constexpr int SL_STEPS = SL_ROWS / 4;   // forward k steps per wave
+constexpr int SL_TILES = SL_ROWS / 16;  // gradient w tiles per wave
+constexpr int SL_TAIL = 64;             // tail floats per wave (Dt <= 2 rows x <= 32 w)
+
+__device__ __forceinline__ sl_f4 sl_mfma(float a, float b, sl_f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+template <int CTRL>
+__device__ __forceinline__ float sl_dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+// 16-lane row sum (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror): every lane of
+// the row ends with the bitwise-identical value
+__device__ __forceinline__ float sl_row_sum16(float v) {
+  v += sl_dpp<0xB1>(v);
+  v += sl_dpp<0x4E>(v);
+  v += sl_dpp<0x141>(v);
+  v += sl_dpp<0x140>(v);
+  return v;
+}
+// xor-16 / xor-32 butterfly steps by v_permlane16/32_swap (no LDS round trip)
+__device__ __forceinline__ float sl_xor16(float v) {
+  const auto q = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(q[0]) + __uint_as_float(q[1]);
+}
+__device__ __forceinline__ float sl_xor32(float v) {
+  const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(q[0]) + __uint_as_float(q[1]);
+}
+__device__ __forceinline__ float sl_groups_sum(float v) { return sl_xor32(sl_xor16(v)); }
+// barrier that leaves LDS-DMA in flight (__syncthreads() would wait vmcnt(0))
+__device__ __forceinline__ void sl_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ uint32_t sl_lds_addr(const float* p) {
+  return (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) float*)p);
+}
+// one 4-B LDS-DMA piece per lane: gsrc -> LDS byte address m0 + 4 * lane (m0 saved / restored)
+__device__ __forceinline__ void sl_dma4(const float* gsrc, const float* lds_dst) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off nt\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(sl_lds_addr(lds_dst)))
+               : "memory");
+}
+// one 16-B LDS-DMA piece per lane: gsrc (4-B aligned is enough) -> LDS byte address m0 + 16 * lane
+__device__ __forceinline__ void sl_dma16(const float* gsrc, const float* lds_dst) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(sl_lds_addr(lds_dst)))
+               : "memory");
+}
+// s_waitcnt vmcnt(n), n wave-uniform in [0, 63]
+__device__ __forceinline__ void sl_wait_vm(int n) {
+#define SL_VM(k) \
+  case k:        \
+    asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); \
+    break;
+#define SL_VM8(b) SL_VM(b) SL_VM(b + 1) SL_VM(b + 2) SL_VM(b + 3) SL_VM(b + 4) SL_VM(b + 5) SL_VM(b + 6) SL_VM(b + 7)
+  switch (n < 0 ? 0 : n) {
+    SL_VM8(0) SL_VM8(8) SL_VM8(16) SL_VM8(24) SL_VM8(32) SL_VM8(40) SL_VM8(48) SL_VM8(56)
+    default:
+      asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
+  }
+#undef SL_VM8
+#undef SL_VM
+}
+// slot xor of chunk r (x = r & 7: bit 0 -> bit 0, bit 1 -> bit 2)
+__device__ __forceinline__ int sl_swz(int x) { return (x & 1) | ((x & 2) << 1); }
+}  // namespace
+
+template <int CC, int DT>
+__global__ __launch_bounds__(SL_T) void k_spec_slice(
+    const float* __restrict__ X, int64_t N, int64_t xld, SpecGeom g, const float* __restrict__ phi,
+    const float* __restrict__ Phi0, const float* __restrict__ wts, const float* __restrict__ y, float scale,
+    float* __restrict__ slab, int64_t slab_stride, double* __restrict__ dpart, float* __restrict__ out,
+    int64_t rows_per_wg, int reverse, const int32_t* __restrict__ stop) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  if (stop != nullptr && *stop != 0) return;
+  const int t = threadIdx.x;
+  const int lane = t & (TR_WAVE - 1);
+  const int wv = __builtin_amdgcn_readfirstlane(t / TR_WAVE);
+  const int p = wv & 3, hw = wv >> 2;
+  const int i = lane & 15, gq = lane >> 4;
+  const int D = g.D, K = g.K, Rn = g.Rn, Rs = g.Rs, NO = g.NO;
+  const int RC = Rs * CC;
+  constexpr int WH = SL_ROWS, ntl = SL_TILES;  // W = 256 (the shapes this kernel is built for)
+  constexpr int Dt = DT;
+  constexpr int TR = WH / 4;   // tail rows of this wave: w offsets [TR p, TR (p + 1)) of its half
+  constexpr int TQ = TR / 16;  // ... = gradient tiles [TQ p, TQ (p + 1))
+  constexpr int SQ = TR / 4;   // ... = forward steps [SQ p, SQ (p + 1))
+  const int wbase = hw * WH;   // first w of this wave's half
+  const int dbase = 32 * p;    // first d of this wave's pair
+  const int rs = i / CC;       // spectral rank of this lane's column (tile 0)
+  const bool rs_ok = rs < Rs;
+  const bool vlane = rs_ok && (i % CC) == 0;  // lane that carries V / dPhi(C1) of rank rs
+
+  float* slice = lds + wv * SL_SLICE;
+  float* sTail = lds + g.sl_oTail + wv * SL_TAIL;  // [Dt][TR]
+  float* sEx = lds + g.sl_oEx;                      // [8 waves][64 lanes][8]
+  float* sTP = lds + g.sl_oTP;                      // [8 waves][2 rows][32 columns]
+  float* sPart = lds + g.sl_oPart;                  // [8 waves][Z 16 | V 16]
+  float* sN1 = lds + g.sl_oN1;                      // [Dp][Rn] phi(A1)
+  float* sC1 = sN1 + g.sl_Dp * Rn;                  // [Dp][Rs] phi(C1)
+  float* sCA = sC1 + g.sl_Dp * Rs;                  // [NO][16] w_r phi(A2)
+  float* sCC = sCA + NO * 16;                       // [NO][16] phi(C2)
+  float* sB = sCC + NO * 16;                        // [NO] bias
+  float* sWt = sB + NO;                             // [16] w_r
+  float* sAcc = sWt + 16;                           // [NO*Rn] dA2 | [NO*Rs] dC2 | [NO] dbias
+  float* sTacc = sAcc + NO * (Rn + Rs + 1);         // wave 0: [Dt][dPhi(A1) 16 | dPhi(C1) 16] of rows 128+
+  double* sLoss = reinterpret_cast<double*>(lds + g.sl_oLoss);  // wave 0 lane 0: sum of squared errors
+
+  for (int e = g.sl_oTail + t; e < g.sl_lds_floats; e += SL_T) lds[e] = 0.f;
+  __syncthreads();
+  for (int e = t; e < D * Rn; e += SL_T) sN1[e] = phi[g.offA1 + e];
+  for (int e = t; e < D * Rs; e += SL_T) sC1[e] = phi[g.offC1 + e];
+  for (int e = t; e < NO * 16; e += SL_T) {
+    const int o = e >> 4, r = e & 15;
+    if (r < Rn) sCA[e] = wts[r] * phi[g.offA2 + o * Rn + r];
+    if (r < Rs) sCC[e] = phi[g.offC2 + o * Rs + r];
+  }
+  for (int e = t; e < NO; e += SL_T) sB[e] = phi[g.offB + e];
+  if (t < Rn) sWt[t] = wts[t];
+
+  // B fragments: lane (i, gq) of step s holds Phi0[wbase + 4 s + gq, column]; tile 0 column i is
+  // spectral column i (Phi0 column Rn + i), tile 1 column i is lin column i
+  float bf0[SL_STEPS], bf1[SL_STEPS];
+#pragma unroll
+  for (int s = 0; s < SL_STEPS; ++s) {
+    const int64_t w = wbase + 4 * s + gq;
+    bf0[s] = i < RC ? Phi0[w * K + Rn + i] : 0.f;
+    bf1[s] = i < Rn ? Phi0[w * K + i] : 0.f;
+  }
+  sl_f4 gacc[SL_TILES][2];
+#pragma unroll
+  for (int q = 0; q < SL_TILES; ++q) {
+    gacc[q][0] = sl_f4{0.f, 0.f, 0.f, 0.f};
+    gacc[q][1] = sl_f4{0.f, 0.f, 0.f, 0.f};
+  }
+  float an1[2][4], as1[4];  // dPhi(A1) partial (both d tiles), dPhi(C1) (own tile h = hw)
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    an1[0][v] = an1[1][v] = 0.f;
+    as1[v] = 0.f;
+  }
+  const float bm = (float)((Rn > 0) + (Rs > 0));  // the bias is added by both terms (Q10)
+
+  // per-lane LDS offsets (floats) of the forward operand (step s: + 128 s, period 4 in the
+  // swizzle) and of the two gradient operand reads (tile q: + 512 q)
+  int fo[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int r = 2 * s + (gq >> 1);
+    fo[s] = 64 * (gq >> 1) + 4 * (((i >> 1) + 8 * (gq & 1)) ^ sl_swz(r)) + 2 * (i & 1);
+  }
+  const int bo0 = 64 * (i >> 1) + 4 * ((2 * gq + 0 + 8 * (i & 1)) ^ sl_swz(i >> 1));
+  const int bo1 = 64 * (i >> 1) + 4 * ((2 * gq + 1 + 8 * (i & 1)) ^ sl_swz(i >> 1));
+
+  const int64_t n0 = (int64_t)blockIdx.x * rows_per_wg;
+  const int64_t n1 = n0 + rows_per_wg < N ? n0 + rows_per_wg : N;
+  const int64_t nr = n1 > n0 ? n1 - n0 : 0;
+  auto sample_of = [&](int64_t k) -> int64_t { return reverse ? (n1 - 1 - k) : (n0 + k); };
+
+  // LDS-DMA of gradient tile q (rows 16q..16q+15 = chunks 8q..8q+7) of this wave's slice of
+  // sample n: two 16-B-per-lane pieces of 4 chunks; lane L fills slot L%16 of chunk 4c4 + L/16,
+  // i.e. row 2r + (slot'>>3), columns 4 (slot' & 7) .. +3 with slot' = (L%16) ^ swz(r & 7).
+  // (global_load_lds_dwordx4 takes 4-B aligned sources; one dword piece per lane costs the
+  // memory pipeline as much as a dwordx4 one: ~3 vs ~6.8 TB/s chip-wide, tools/ldsdma_probe.hip.)
+  // The per-lane offsets are recomputed from an opaque copy of the lane index at every call:
+  // hoisted out of the sample loop they would hold 16 address registers.
+  auto dma_tile = [&](int64_t n, int q) {
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int lsl = ln & 15, lc = ln >> 4;
+    const float* src = X + n * xld + (int64_t)(wbase + 16 * q) * D;
+#pragma unroll
+    for (int c4 = 0; c4 < 2; ++c4) {
+      const int x = 4 * c4 + lc;  // chunk within the tile (= r & 7)
+      const int sp = lsl ^ sl_swz(x);
+      int d = dbase + 4 * (sp & 7);
+      d = d < D ? d : 0;  // a column quad past D (D < 128, D % 4 == 0): any valid quad, times zero
+      sl_dma16(src + ((2 * x + (sp >> 3)) * D + d), slice + 64 * (8 * q + 4 * c4));
+    }
+  };
+  auto dma_tail = [&](int64_t n) {
+    if (lane < Dt * TR) {  // lane -> (row 128 + lane / TR, w offset lane % TR)
+      const int tr = lane / TR, wo = lane - tr * TR;
+      const int64_t w = wbase + TR * p + wo;
+      sl_dma4(X + n * xld + w * D + 128 + tr, sTail);
+    }
+  };
+  auto dma_sample = [&](int64_t n) {  // tail first: waiting for tile 0 also retires it
+    if (Dt > 0) dma_tail(n);
+#pragma unroll
+    for (int q = 0; q < SL_TILES; ++q) dma_tile(n, q);
+  };
+
+  __builtin_amdgcn_s_waitcnt(0);  // retire the prologue's loads (the loop's waits are counted)
+  __syncthreads();
+  if (nr > 0) dma_sample(sample_of(0));
+#if TR_SLICE_PROFILE
+  unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long prof_t = __builtin_readcyclecounter();
+#endif
+
+#pragma unroll 1
+  for (int64_t k = 0; k < nr; ++k) {
+    const int64_t n = sample_of(k);
+    const bool has_next = k + 1 < nr && !((TR_SLICE_SKIP & 1) && k > 0);
+    const int64_t nn = has_next ? sample_of(k + 1) : n;
+
+    // ---- forward: T (tile jt, d tile h) over this wave's half ---------------------------
+    sl_f4 T00 = {0.f, 0.f, 0.f, 0.f}, T01 = T00, T10 = T00, T11 = T00;
+    // tail rows d = 128 + tr: VALU partial over this wave's tail steps [SQ p, SQ (p + 1)) inside
+    // the forward loop (bf0 / bf1 of the step are in hand), reduced over lane groups after it
+    float ta[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
+    {
+      sl_f2 xa[4], xb[4];
+      {
+        SL_SUB_BEGIN();
+        sl_wait_vm((ntl - 1) * 2);
+        SL_SUB_END(1);
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s) xa[s] = *reinterpret_cast<const sl_f2*>(slice + 128 * s + fo[s]);
+#pragma unroll
+      for (int q = 0; q < SL_TILES; ++q) {
+        if (q + 1 < ntl) {
+          {
+            SL_SUB_BEGIN();
+            sl_wait_vm((ntl - 2 - q) * 2);
+            SL_SUB_END(1);
+          }
+#pragma unroll
+          for (int s = 0; s < 4; ++s)
+            xb[s] = *reinterpret_cast<const sl_f2*>(slice + 128 * (4 * (q + 1) + s) + fo[s]);
+        }
+#pragma unroll
+        for (int s = 0; s < 4 && !(TR_SLICE_SKIP & 2); ++s) {
+          T00 = sl_mfma(xa[s].x, bf0[4 * q + s], T00);
+          T01 = sl_mfma(xa[s].y, bf0[4 * q + s], T01);
+          T10 = sl_mfma(xa[s].x, bf1[4 * q + s], T10);
+          T11 = sl_mfma(xa[s].y, bf1[4 * q + s], T11);
+        }
+        if (Dt > 0 && q / TQ == p) {
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            const int wo = 4 * (4 * q + s - SQ * p) + gq;
+#pragma unroll
+            for (int tr = 0; tr < Dt; ++tr) {
+              const float xt = sTail[tr * TR + wo];
+              ta[tr][0] = fmaf(xt, bf0[4 * q + s], ta[tr][0]);
+              ta[tr][1] = fmaf(xt, bf1[4 * q + s], ta[tr][1]);
+            }
+          }
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) xa[s] = xb[s];
+      }
+    }
+    if (Dt > 0) {
+#pragma unroll
+      for (int tr = 0; tr < Dt; ++tr) {
+        ta[tr][0] = sl_groups_sum(ta[tr][0]);
+        ta[tr][1] = sl_groups_sum(ta[tr][1]);
+        if (gq == 0) {
+          sTP[(wv * 2 + tr) * 32 + i] = ta[tr][0];
+          sTP[(wv * 2 + tr) * 32 + 16 + i] = ta[tr][1];
+        }
+      }
+    }
+    SL_MARK(0);
+    // ---- exchange the spectral tiles with the partner half ---------------------------------
+    *reinterpret_cast<sl_f4*>(sEx + (wv * TR_WAVE + lane) * 8) = T00;
+    *reinterpret_cast<sl_f4*>(sEx + (wv * TR_WAVE + lane) * 8 + 4) = T01;
+    SL_MARK(2);
+    sl_barrier();
+    SL_MARK(3);
+    {
+      const float* pe = sEx + ((wv ^ 4) * TR_WAVE + lane) * 8;
+      T00 += *reinterpret_cast<const sl_f4*>(pe);  // two-term sums commute: both halves hold
+      T01 += *reinterpret_cast<const sl_f4*>(pe + 4);  // the bitwise-identical full tile
+    }
+    // full tail row values: lane (i, gq < Dt) holds T[128 + gq][spectral i] / [lin i]
+    float tt0 = 0.f, tt1 = 0.f;
+    if (Dt > 0 && gq < Dt) {
+#pragma unroll
+      for (int w2 = 0; w2 < SL_NW; ++w2) {
+        tt0 += sTP[(w2 * 2 + gq) * 32 + i];
+        tt1 += sTP[(w2 * 2 + gq) * 32 + 16 + i];
+      }
+    }
+
+    // y of this sample, lane o (n_out <= 64); read by readlane after barrier B
+    const float yv = lane < NO ? y[n * NO + lane] : 0.f;
+
+    // ---- column partials: Z (lin, both d tiles, this half's partial T) and V (spectral, own d
+    // tile h = hw, full T) -- nothing but the two sums stays live across barrier B -------------
+    auto norm_of = [&](float x) {  // || T[d, spectral group of this lane] ||
+      float sq = x * x;
+      if (CC >= 2) sq += sl_dpp<0xB1>(sq);
+      if (CC >= 4) sq += sl_dpp<0x4E>(sq);
+      return __builtin_amdgcn_sqrtf(sq);
+    };
+    // table offsets from an opaque copy of the lane index: recomputed here (a few VALU ops)
+    // instead of living across the sample loop as spilled registers
+    int lo = lane;
+    asm volatile("" : "+v"(lo));
+    const int ie = lo & 15, ge = lo >> 4, rse = ie / CC;
+    const int n1o = 8 * ge * Rn + ie, c1o = 8 * ge * Rs + rse;  // + d' * Rn / Rs
+    auto drow = [&](int h, int v) { return dbase + 2 * v + h; };  // (+ 8 gq, folded into n1o / c1o)
+    float zp = 0.f, vp = 0.f;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) zp = fmaf(i < Rn ? sN1[drow(h, v) * Rn + n1o] : 0.f, h == 0 ? T10[v] : T11[v], zp);
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+      vp = fmaf(rs_ok ? sC1[drow(hw, v) * Rs + c1o] : 0.f, norm_of(hw == 0 ? T00[v] : T01[v]), vp);
+    vp = vlane ? vp : 0.f;
+    const float Mt = norm_of(tt0);
+    const int dtl = 128 + gq;  // tail row of this lane group (valid when gq < Dt)
+    const float n1t = (Dt > 0 && gq < Dt && i < Rn) ? sN1[dtl * Rn + i] : 0.f;
+    const float c1t = (Dt > 0 && gq < Dt && rs_ok) ? sC1[dtl * Rs + rs] : 0.f;
+    zp = sl_groups_sum(zp);
+    vp = sl_groups_sum(vp);
+    if (wv == 0 && Dt > 0) {  // wave 0 adds the tail rows' terms
+      float zt = n1t * tt1;
+      float vt = vlane ? c1t * Mt : 0.f;
+      zp += sl_groups_sum(zt);
+      vp += sl_groups_sum(vt);
+    }
+    if (gq == 0) {
+      sPart[wv * 32 + i] = zp;
+      if (vlane) sPart[wv * 32 + 16 + rs] = vp;
+    }
+    SL_MARK(4);
+    sl_barrier();
+    SL_MARK(5);
+
+    // ---- Z / V, y_hat, residual, dZ / dV (every wave, identical order) ----------------------
+    float zi = 0.f, vi = 0.f;
+#pragma unroll
+    for (int w2 = 0; w2 < SL_NW; ++w2) {
+      zi += sPart[w2 * 32 + i];
+      vi += sPart[w2 * 32 + 16 + i];
+    }
+    float dz = 0.f, dv = 0.f;
+    for (int o = 0; o < NO; ++o) {
+      const float ca = sCA[o * 16 + i], cc = sCC[o * 16 + i];
+      const float pl = sl_row_sum16(ca * zi);
+      const float ps = sl_row_sum16(cc * vi);
+      const float b = sB[o];
+      const float yh = (Rn > 0 ? pl + b : 0.f) + (Rs > 0 ? ps + b : 0.f);
+      const float e = yh - __int_as_float(__builtin_amdgcn_readlane(__float_as_int(yv), o));
+      const float rv = e * scale;
+      dz = fmaf(rv, ca, dz);
+      dv = fmaf(rv, sCC[o * 16 + rs], dv);
+      if (wv == 0 && lane < 16) {
+        if (i < Rn) sAcc[o * Rn + i] += sWt[i] * rv * zi;
+        if (i < Rs) sAcc[NO * Rn + o * Rs + i] += rv * vi;
+        if (lane == 0) {
+          sAcc[NO * (Rn + Rs) + o] += bm * rv;
+          *sLoss += (double)e * (double)e;
+          if (out != nullptr) out[n * NO + o] = yh;
+        }
+      }
+    }
+    dz = i < Rn ? dz : 0.f;
+    dv = rs_ok ? dv : 0.f;
+
+    // ---- dT (in place, accumulator layout = gradient B operand) and dPhi(A1) / dPhi(C1) -----
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const float m0 = norm_of(T00[v]), m1 = norm_of(T01[v]);
+      const float c10 = rs_ok ? sC1[drow(0, v) * Rs + c1o] : 0.f, c11 = rs_ok ? sC1[drow(1, v) * Rs + c1o] : 0.f;
+      an1[0][v] = fmaf(dz, T10[v], an1[0][v]);
+      an1[1][v] = fmaf(dz, T11[v], an1[1][v]);
+      as1[v] = fmaf(dv, hw == 0 ? m0 : m1, as1[v]);
+      T10[v] = dz * (i < Rn ? sN1[drow(0, v) * Rn + n1o] : 0.f);
+      T11[v] = dz * (i < Rn ? sN1[drow(1, v) * Rn + n1o] : 0.f);
+      const float q0 = m0 > 0.f ? dv * c10 * __builtin_amdgcn_rcpf(m0) : 0.f;
+      const float q1 = m1 > 0.f ? dv * c11 * __builtin_amdgcn_rcpf(m1) : 0.f;
+      T00[v] = q0 * T00[v];
+      T01[v] = q1 * T01[v];
+    }
+    float dTt0 = 0.f, dTt1 = 0.f;  // tail rows: B operand of the zero-padded gradient k step
+    if (Dt > 0) {
+      dTt1 = dz * n1t;
+      dTt0 = Mt > 0.f ? dv * c1t * __builtin_amdgcn_rcpf(Mt) * tt0 : 0.f;
+      if (wv == 0 && gq < Dt) {
+        if (i < Rn) sTacc[gq * 32 + i] = fmaf(dz, tt1, sTacc[gq * 32 + i]);
+        if (vlane) sTacc[gq * 32 + 16 + rs] = fmaf(dv, Mt, sTacc[gq * 32 + 16 + rs]);
+      }
+    }
+
+    SL_MARK(6);
+    // ---- gradient: dPhi0[w in half, :] += X[w, d in pair] dT[d in pair, :] ------------------
+    {
+      // tail operands of tiles TQ p, TQ p + 1 (then the tail rows are free for the next sample)
+      float at[TQ];
+#pragma unroll
+      for (int u = 0; u < TQ; ++u) at[u] = (Dt > 0 && gq < Dt) ? sTail[gq * TR + 16 * u + i] : 0.f;
+      if (has_next && Dt > 0) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        dma_tail(nn);
+      }
+#pragma unroll
+      for (int q = 0; q < SL_TILES; ++q) {
+        if (q < ntl) {
+          const sl_f4 va = *reinterpret_cast<const sl_f4*>(slice + 512 * q + bo0);
+          const sl_f4 vb = *reinterpret_cast<const sl_f4*>(slice + 512 * q + bo1);
+#pragma unroll
+          for (int v = 0; v < 4 && !(TR_SLICE_SKIP & 4); ++v) {
+            const sl_f4& src = v < 2 ? va : vb;
+            const float a0 = src[2 * (v & 1) + 0], a1 = src[2 * (v & 1) + 1];
+            gacc[q][0] = sl_mfma(a0, T00[v], gacc[q][0]);
+            gacc[q][1] = sl_mfma(a0, T10[v], gacc[q][1]);
+            gacc[q][0] = sl_mfma(a1, T01[v], gacc[q][0]);
+            gacc[q][1] = sl_mfma(a1, T11[v], gacc[q][1]);
+          }
+          if (Dt > 0 && q / TQ == p) {
+            gacc[q][0] = sl_mfma(at[q % TQ], dTt0, gacc[q][0]);
+            gacc[q][1] = sl_mfma(at[q % TQ], dTt1, gacc[q][1]);
+          }
+          if (has_next) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // tile q's reads have landed
+            dma_tile(nn, q);
+          }
+        }
+      }
+    }
+    SL_MARK(7);
+  }
+
+#if TR_SLICE_PROFILE
+  if (lane == 0 && blockIdx.x < 256)
+    for (int q = 0; q < 8; ++q) g_slice_prof[blockIdx.x][wv][q] = prof[q];
+#endif
+  // ---- per-workgroup slab (arena layout, phi space) -------------------------------------------
+  __syncthreads();  // (no LDS-DMA in flight: the last sample issued none)
+#pragma unroll
+  for (int q = 0; q < SL_TILES; ++q)
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt) *reinterpret_cast<sl_f4*>(slice + ((q * 2 + jt) * TR_WAVE + lane) * 4) = gacc[q][jt];
+  *reinterpret_cast<sl_f4*>(sEx + (wv * TR_WAVE + lane) * 8) = sl_f4{an1[0][0], an1[0][1], an1[0][2], an1[0][3]};
+  *reinterpret_cast<sl_f4*>(sEx + (wv * TR_WAVE + lane) * 8 + 4) = sl_f4{an1[1][0], an1[1][1], an1[1][2], an1[1][3]};
+  __syncthreads();
+  float* sl = slab + (int64_t)blockIdx.x * slab_stride;
+  // dPhi0 (A0 and C0 columns): the four pairs' partials in pair order
+  for (int e = t; e < g.W * 32; e += SL_T) {
+    const int w = e >> 5, jc = e & 31;
+    const int h2 = w / WH, wl = w - h2 * WH;
+    const int q = wl >> 4, gg = (wl & 15) >> 2, reg = wl & 3, jt = jc >> 4, ii = jc & 15;
+    const int idx = ((q * 2 + jt) * TR_WAVE + 16 * gg + ii) * 4 + reg;
+    float s = 0.f;
+#pragma unroll
+    for (int p2 = 0; p2 < 4; ++p2) s += lds[(p2 + 4 * h2) * SL_SLICE + idx];
+    if (jt == 0) {
+      if (ii < RC) sl[g.offC0 + (int64_t)w * RC + ii] = s;
+    } else if (ii < Rn) {
+      sl[g.offA0 + (int64_t)w * Rn + ii] = s;
+    }
+  }
+  // dPhi(A1) rows d < 128: the two halves' partials; dPhi(C1): the owner lane's own sum
+  const int Dm = D < 128 ? D : 128;
+  for (int e = t; e < Dm * Rn; e += SL_T) {
+    const int d = e / Rn, r = e - d * Rn;
+    const int p2 = d >> 5, c = d & 31, gg = c >> 3, v = (c & 7) >> 1, h = c & 1;
+    const int li = 16 * gg + r;
+    sl[g.offA1 + e] = sEx[(p2 * TR_WAVE + li) * 8 + 4 * h + v] + sEx[((p2 + 4) * TR_WAVE + li) * 8 + 4 * h + v];
+  }
+  if (vlane) {
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int d = dbase + 8 * gq + 2 * v + hw;
+      if (d < D) sl[g.offC1 + (int64_t)d * Rs + rs] = as1[v];
+    }
+  }
+  if (wv == 0 && Dt > 0 && gq < Dt) {
+    if (i < Rn) sl[g.offA1 + (int64_t)(128 + gq) * Rn + i] = sTacc[gq * 32 + i];
+    if (vlane) sl[g.offC1 + (int64_t)(128 + gq) * Rs + rs] = sTacc[gq * 32 + 16 + rs];
+  }
+  for (int e = t; e < NO * Rn; e += SL_T) sl[g.offA2 + e] = sAcc[e];
+  for (int e = t; e < NO * Rs; e += SL_T) sl[g.offC2 + e] = sAcc[NO * Rn + e];
+  for (int e = t; e < NO; e += SL_T) sl[g.offB + e] = sAcc[NO * (Rn + Rs) + e];
+  if (t == 0) {
+    dpart[2 * blockIdx.x] = *sLoss;
+    dpart[2 * blockIdx.x + 1] = 0.0;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------------------------
+void spec_slice_geom(SpecGeom* g) {
+  g->sl = 0;
+  const char* env = std::getenv("TR_SPEC_SLICE");
+  if (env != nullptr && env[0] == '0') return;
+  const char* gen = std::getenv("TR_SPEC_GENERIC");  // forcing the generic path forces it for training too
+  if (gen != nullptr && gen[0] == '1') return;
+  if (g->Rn < 1 || g->Rn > 16 || g->Rs < 1 || g->Rs * g->Cc > 16) return;
+  if (!(g->Cc == 1 || g->Cc == 2 || g->Cc == 4)) return;
+  if (g->W != 2 * SL_ROWS) return;
+  if (g->D < 97 || g->D > 130 || (g->D < 128 && g->D % 4 != 0)) return;  // whole column quads
+  const int Dt = g->D > 128 ? g->D - 128 : 0;
+  if (g->NO > 64) return;
+  g->slDt = Dt;
+  g->sl_Dp = g->D > 128 ? g->D : 128;
+  g->sl_oTail = SL_NW * SL_SLICE;
+  g->sl_oEx = g->sl_oTail + SL_NW * SL_TAIL;
+  g->sl_oTP = g->sl_oEx + SL_NW * TR_WAVE * 8;
+  g->sl_oPart = g->sl_oTP + SL_NW * 64;
+  g->sl_oN1 = g->sl_oPart + SL_NW * 32;
+  const int64_t small = (int64_t)g->sl_Dp * (g->Rn + g->Rs) + (int64_t)g->NO * 33 + 16 +
+                        (int64_t)g->NO * (g->Rn + g->Rs + 1) + 2 * 32;
+  g->sl_oLoss = (int)(g->sl_oN1 + ((small + 3) & ~(int64_t)3));  // 16-B aligned double
+  const int64_t tot = g->sl_oLoss + 4;
+  if (tot * 4 > 160 * 1024) return;
+  g->sl_lds_floats = (int)tot;
+  g->sl = 1;
+}
+
+template <int DT>
+static const void* slice_kernel_dt(int cc) {
+  if (cc == 1) return reinterpret_cast<const void*>(&k_spec_slice<1, DT>);
+  if (cc == 2) return reinterpret_cast<const void*>(&k_spec_slice<2, DT>);
+  return reinterpret_cast<const void*>(&k_spec_slice<4, DT>);
+}
+static const void* slice_kernel(int cc, int dt) {
+  return dt == 0 ? slice_kernel_dt<0>(cc) : (dt == 1 ? slice_kernel_dt<1>(cc) : slice_kernel_dt<2>(cc));
+}
+
+hipError_t spec_slice_prepare(SpecGeom* g) {
+  if (!g->sl) return hipSuccess;
+  const void* k = slice_kernel(g->Cc, g->slDt);
+  hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, g->sl_lds_floats * 4);
+  if (e != hipSuccess) return e;
+  int per_cu = 0;
+  e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, SL_T, (size_t)g->sl_lds_floats * 4);
+  if (e != hipSuccess) return e;
+  if (per_cu < 1) g->sl = 0;  // falls back to k_spec_fused
+  return hipSuccess;
+}
+
+hipError_t launch_spec_slice(const SpecGeom& g, int grid, const float* X, int64_t N, int64_t xld, const float* phi,
+                             const float* Phi0, const float* wts, const float* y, float scale, float* slab,
+                             int64_t slab_stride, double* dpart, float* out, int64_t rows_per_wg, int reverse,
+                             const int32_t* stop, hipStream_t st) {
+  const size_t lb = (size_t)g.sl_lds_floats * 4;
+#define SL_LAUNCH(C, T)                                                                                          \
+  hipLaunchKernelGGL((k_spec_slice<C, T>), dim3(grid), dim3(SL_T), lb, st, X, N, xld, g, phi, Phi0, wts, y, scale, \
+                     slab, slab_stride, dpart, out, rows_per_wg, reverse, stop)
+#define SL_LAUNCH_CC(T) \
+  if (g.Cc == 1)        \
+    SL_LAUNCH(1, T);    \
+  else if (g.Cc == 2)   \
+    SL_LAUNCH(2, T);    \
+  else                  \
+    SL_LAUNCH(4, T);
+  if (g.slDt == 0) {
+    SL_LAUNCH_CC(0)
+  } else if (g.slDt == 1) {
+    SL_LAUNCH_CC(1)
+  } else {
+    SL_LAUNCH_CC(2)
+  }
+#undef SL_LAUNCH_CC
+#undef SL_LAUNCH
+  return hipGetLastError();
+}
+
+#if TR_SLICE_PROFILE
+}  // namespace tr
+extern "C" int tr_slice_profile_read(unsigned long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(tr::g_slice_prof), sizeof(tr::g_slice_prof));
+}
+namespace tr {
+#endif
+}  // namespace tr

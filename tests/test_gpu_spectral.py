@@ -26,15 +26,21 @@ def spec_path(kind):
     force the three-kernel path (TR_SPEC_GENERIC=1, read at plan creation)."""
     from tensor_regression_amd import spectral_tensor_regression as SP
     old = os.environ.pop("TR_SPEC_GENERIC", None)
+    old_sl = os.environ.pop("TR_SPEC_SLICE", None)
     if kind == "generic":
         os.environ["TR_SPEC_GENERIC"] = "1"
+    if kind == "lockstep":  # the whole-sample lock-step kernel where the column-slice one would run
+        os.environ["TR_SPEC_SLICE"] = "0"
     SP._plan_cache.clear()
     try:
         yield
     finally:
         os.environ.pop("TR_SPEC_GENERIC", None)
+        os.environ.pop("TR_SPEC_SLICE", None)
         if old is not None:
             os.environ["TR_SPEC_GENERIC"] = old
+        if old_sl is not None:
+            os.environ["TR_SPEC_SLICE"] = old_sl
         SP._plan_cache.clear()
 
 pytestmark = pytest.mark.gpu
@@ -181,6 +187,16 @@ SHAPES = [
     (77, 17, 7, 2, 0, 4, 1, [False, False, False]),       # rank_normal = 0
     (77, 17, 7, 2, 3, 0, 1, [False, False, False]),       # rank_spectral = 0
 ]
+# shapes of the column-slice training kernel (csrc/tr_spectral_slice.hip: W = 256, 97 <= D <= 130,
+# Rn <= 16, Rs * Cc <= 16, Cc in {1, 2, 4}): every variant of its tail rows (D - 128 = 0, 1, 2),
+# masked columns (D < 128) and norm groups
+SLICE_SHAPES = [
+    (200, 256, 128, 3, 8, 4, 3, [False, True, False]),    # Cc = 4, Rs * Cc = 16, no tail rows
+    (150, 256, 130, 2, 8, 8, 0, [True, False, True]),     # Cc = 1, two tail rows
+    (120, 256, 100, 5, 3, 5, 1, [False, False, False]),   # D < 128 (columns past D masked)
+    (64, 256, 129, 8, 8, 8, 1, [False, False, False]),    # n_out = 8
+    (64, 256, 129, 40, 8, 8, 1, [False, False, False]),   # n_out = 40: beyond the slice kernel's LDS
+]
 # beyond the fused kernel's envelope: the generic path whatever TR_SPEC_GENERIC says
 WIDE_SHAPES = [
     (40, 300, 257, 3, 4, 5, 1, [False, True, False]),     # W > 256 and D > 256
@@ -190,8 +206,24 @@ WIDE_SHAPES = [
 ]
 
 
+def _slice_shape(W, D, Rn, Rs, ncd, O):
+    """the column-slice kernel's envelope (spec_slice_geom in csrc/tr_spectral_slice.hip)"""
+    ok = (W == 256 and 97 <= D <= 130 and (D >= 128 or D % 4 == 0) and 1 <= Rn <= 16 and Rs >= 1
+          and Rs * (ncd + 1) <= 16 and ncd + 1 in (1, 2, 4) and O <= 64)
+    small = max(D, 128) * (Rn + Rs) + O * 33 + 16 + O * (Rn + Rs + 1) + 64
+    return ok and (38144 + ((small + 3) & ~3) + 4) * 4 <= 160 * 1024
+
+
+@pytest.mark.parametrize("kind", ["lockstep"])
+@pytest.mark.parametrize("N,W,D,O,Rn,Rs,ncd,nn", [SHAPES[0]] + SLICE_SHAPES)
+def test_spectral_slice_shapes_lockstep_kernel(N, W, D, O, Rn, Rs, ncd, nn, kind):
+    """the same shapes through the whole-sample lock-step kernel (TR_SPEC_SLICE=0)"""
+    with spec_path(kind):
+        _spectral_shape(N, W, D, O, Rn, Rs, ncd, nn, kind)
+
+
 @pytest.mark.parametrize("kind", ["fused", "generic"])
-@pytest.mark.parametrize("N,W,D,O,Rn,Rs,ncd,nn", SHAPES + WIDE_SHAPES)
+@pytest.mark.parametrize("N,W,D,O,Rn,Rs,ncd,nn", SHAPES + SLICE_SHAPES + WIDE_SHAPES)
 def test_spectral_shapes_vs_closed_form(N, W, D, O, Rn, Rs, ncd, nn, kind):
     if kind == "fused" and (N, W, D, O, Rn, Rs, ncd, nn) in WIDE_SHAPES:
         pytest.skip("beyond the fused envelope: covered by the generic case")
@@ -217,7 +249,9 @@ def _spectral_shape(N, W, D, O, Rn, Rs, ncd, nn, kind):
     Xd, yd = X.to(DEV), y.to(DEV)
     plan = model._get_plan(Xd, N)
     wide = W > 256 or D > 256 or O > 256 or Rn + Rs * (ncd + 1) > 32
-    assert ("generic" in plan.describe) == (kind == "generic" or wide), plan.describe
+    if kind == "generic" or (kind == "fused" and wide):
+        assert "generic" in plan.describe, plan.describe
+    assert ("slice" in plan.describe) == (kind == "fused" and _slice_shape(W, D, Rn, Rs, ncd, O)), plan.describe
     arena = plan.pack(model.Bcp_n, model.Bcp_c, model.bias)
     w = torch.ones(Rn + Rs, device=DEV)
     grad = torch.zeros(plan.num_grads, device=DEV)
@@ -250,7 +284,7 @@ def _spectral_shape(N, W, D, O, Rn, Rs, ncd, nn, kind):
         assert normwise_rel(lat, ref_lat) <= RTOL
 
 
-@pytest.mark.parametrize("kind", ["fused", "generic"])
+@pytest.mark.parametrize("kind", ["fused", "lockstep", "generic"])
 def test_spectral_bitwise_reproducible_and_sharded_sum(kind):
     with spec_path(kind):
         _spectral_bitwise(kind)
