@@ -45,6 +45,12 @@
 #define TR_SLICE_SKIP 0  // timing ablation only (results invalid): 1 no LDS-DMA after the first sample,
                          // 2 no forward MFMAs, 4 no gradient MFMAs
 #endif
+#ifndef TR_SLICE_PRIO
+#define TR_SLICE_PRIO 1  // s_setprio 1 for the second-dispatched half (waves 4-7)
+#endif
+#ifndef TR_SLICE_BPF
+#define TR_SLICE_BPF 1  // gradient GEMM: next tile's operand reads issued before this tile's MFMAs
+#endif
 #ifndef TR_SLICE_PROFILE
 #define TR_SLICE_PROFILE 0  // profiling build: per-phase cycle counts of wave 0 of workgroups 0..255
 #endif
@@ -185,8 +191,9 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
   float* sEx = lds + g.sl_oEx;                      // [8 waves][64 lanes][8]
   float* sTP = lds + g.sl_oTP;                      // [8 waves][2 rows][32 columns]
   float* sPart = lds + g.sl_oPart;                  // [8 waves][Z 16 | V 16]
-  float* sN1 = lds + g.sl_oN1;                      // [Dp][Rn] phi(A1)
-  float* sC1 = sN1 + g.sl_Dp * Rn;                  // [Dp][Rs] phi(C1)
+  const int Dp = g.sl_Dp;                           // table row length (>= max(D, 128), % 4 == 0)
+  float* sN1 = lds + g.sl_oN1;                      // [Rn][Dp] phi(A1)^T (d contiguous: b128 reads)
+  float* sC1 = sN1 + Dp * Rn;                       // [Rs][Dp] phi(C1)^T
   float* sCA = sC1 + g.sl_Dp * Rs;                  // [NO][16] w_r phi(A2)
   float* sCC = sCA + NO * 16;                       // [NO][16] phi(C2)
   float* sB = sCC + NO * 16;                        // [NO] bias
@@ -197,8 +204,8 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
 
   for (int e = g.sl_oTail + t; e < g.sl_lds_floats; e += SL_T) lds[e] = 0.f;
   __syncthreads();
-  for (int e = t; e < D * Rn; e += SL_T) sN1[e] = phi[g.offA1 + e];
-  for (int e = t; e < D * Rs; e += SL_T) sC1[e] = phi[g.offC1 + e];
+  for (int e = t; e < D * Rn; e += SL_T) sN1[(e % Rn) * Dp + e / Rn] = phi[g.offA1 + e];
+  for (int e = t; e < D * Rs; e += SL_T) sC1[(e % Rs) * Dp + e / Rs] = phi[g.offC1 + e];
   for (int e = t; e < NO * 16; e += SL_T) {
     const int o = e >> 4, r = e & 15;
     if (r < Rn) sCA[e] = wts[r] * phi[g.offA2 + o * Rn + r];
@@ -253,19 +260,20 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
   // memory pipeline as much as a dwordx4 one: ~3 vs ~6.8 TB/s chip-wide, tools/ldsdma_probe.hip.)
   // The per-lane offsets are recomputed from an opaque copy of the lane index at every call:
   // hoisted out of the sample loop they would hold 16 address registers.
-  auto dma_tile = [&](int64_t n, int q) {
+  auto dma_piece = [&](int64_t n, int q, int c4) {  // chunks 8q + 4c4 .. +3
     int ln = lane;
     asm volatile("" : "+v"(ln));
     const int lsl = ln & 15, lc = ln >> 4;
     const float* src = X + n * xld + (int64_t)(wbase + 16 * q) * D;
-#pragma unroll
-    for (int c4 = 0; c4 < 2; ++c4) {
-      const int x = 4 * c4 + lc;  // chunk within the tile (= r & 7)
-      const int sp = lsl ^ sl_swz(x);
-      int d = dbase + 4 * (sp & 7);
-      d = d < D ? d : 0;  // a column quad past D (D < 128, D % 4 == 0): any valid quad, times zero
-      sl_dma16(src + ((2 * x + (sp >> 3)) * D + d), slice + 64 * (8 * q + 4 * c4));
-    }
+    const int x = 4 * c4 + lc;  // chunk within the tile (= r & 7)
+    const int sp = lsl ^ sl_swz(x);
+    int d = dbase + 4 * (sp & 7);
+    d = d < D ? d : 0;  // a column quad past D (D < 128, D % 4 == 0): any valid quad, times zero
+    sl_dma16(src + ((2 * x + (sp >> 3)) * D + d), slice + 64 * (8 * q + 4 * c4));
+  };
+  auto dma_tile = [&](int64_t n, int q) {
+    dma_piece(n, q, 0);
+    dma_piece(n, q, 1);
   };
   auto dma_tail = [&](int64_t n) {
     if (lane < Dt * TR) {  // lane -> (row 128 + lane / TR, w offset lane % TR)
@@ -283,6 +291,7 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
   __builtin_amdgcn_s_waitcnt(0);  // retire the prologue's loads (the loop's waits are counted)
   __syncthreads();
   if (nr > 0) dma_sample(sample_of(0));
+  if (TR_SLICE_PRIO && hw == 1) __builtin_amdgcn_s_setprio(1);
 #if TR_SLICE_PROFILE
   unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long prof_t = __builtin_readcyclecounter();
@@ -392,21 +401,34 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
     int lo = lane;
     asm volatile("" : "+v"(lo));
     const int ie = lo & 15, ge = lo >> 4, rse = ie / CC;
-    const int n1o = 8 * ge * Rn + ie, c1o = 8 * ge * Rs + rse;  // + d' * Rn / Rs
-    auto drow = [&](int h, int v) { return dbase + 2 * v + h; };  // (+ 8 gq, folded into n1o / c1o)
+    // phi(A1)[d, ie] / phi(C1)[d, ie / CC] of this lane's 8 rows d = dbase + 8 ge + 2v + h: two
+    // ds_read_b128 each, element 2v + h
+    const int n1o = (ie < Rn ? ie : 0) * Dp + dbase + 8 * ge, c1o = (rse < Rs ? rse : 0) * Dp + dbase + 8 * ge;
+    auto tab8 = [&](const float* tb, int off, bool ok, float (&o)[2][4]) {
+      const sl_f4 lo = *reinterpret_cast<const sl_f4*>(tb + off), hi = *reinterpret_cast<const sl_f4*>(tb + off + 4);
+#pragma unroll
+      for (int v = 0; v < 4; ++v)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) o[h][v] = ok ? (v < 2 ? lo[2 * v + h] : hi[2 * (v - 2) + h]) : 0.f;
+    };
     float zp = 0.f, vp = 0.f;
+    {
+      float n1[2][4], c1[2][4];
+      tab8(sN1, n1o, i < Rn, n1);
+      tab8(sC1, c1o, rs_ok, c1);
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+      for (int h = 0; h < 2; ++h)
 #pragma unroll
-      for (int v = 0; v < 4; ++v) zp = fmaf(i < Rn ? sN1[drow(h, v) * Rn + n1o] : 0.f, h == 0 ? T10[v] : T11[v], zp);
+        for (int v = 0; v < 4; ++v) zp = fmaf(n1[h][v], h == 0 ? T10[v] : T11[v], zp);
 #pragma unroll
-    for (int v = 0; v < 4; ++v)
-      vp = fmaf(rs_ok ? sC1[drow(hw, v) * Rs + c1o] : 0.f, norm_of(hw == 0 ? T00[v] : T01[v]), vp);
+      for (int v = 0; v < 4; ++v)
+        vp = fmaf(hw == 0 ? c1[0][v] : c1[1][v], norm_of(hw == 0 ? T00[v] : T01[v]), vp);
+    }
     vp = vlane ? vp : 0.f;
     const float Mt = norm_of(tt0);
     const int dtl = 128 + gq;  // tail row of this lane group (valid when gq < Dt)
-    const float n1t = (Dt > 0 && gq < Dt && i < Rn) ? sN1[dtl * Rn + i] : 0.f;
-    const float c1t = (Dt > 0 && gq < Dt && rs_ok) ? sC1[dtl * Rs + rs] : 0.f;
+    const float n1t = (Dt > 0 && gq < Dt && i < Rn) ? sN1[i * Dp + dtl] : 0.f;
+    const float c1t = (Dt > 0 && gq < Dt && rs_ok) ? sC1[rs * Dp + dtl] : 0.f;
     zp = sl_groups_sum(zp);
     vp = sl_groups_sum(vp);
     if (wv == 0 && Dt > 0) {  // wave 0 adds the tail rows' terms
@@ -424,6 +446,9 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
     SL_MARK(5);
 
     // ---- Z / V, y_hat, residual, dZ / dV (every wave, identical order) ----------------------
+    float n1[2][4], c1[2][4];  // (issued first: their latency hides under the sums below)
+    tab8(sN1, n1o, i < Rn, n1);
+    tab8(sC1, c1o, rs_ok, c1);
     float zi = 0.f, vi = 0.f;
 #pragma unroll
     for (int w2 = 0; w2 < SL_NW; ++w2) {
@@ -431,6 +456,7 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
       vi += sPart[w2 * 32 + 16 + i];
     }
     float dz = 0.f, dv = 0.f;
+#pragma unroll 2
     for (int o = 0; o < NO; ++o) {
       const float ca = sCA[o * 16 + i], cc = sCC[o * 16 + i];
       const float pl = sl_row_sum16(ca * zi);
@@ -458,12 +484,12 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
       const float m0 = norm_of(T00[v]), m1 = norm_of(T01[v]);
-      const float c10 = rs_ok ? sC1[drow(0, v) * Rs + c1o] : 0.f, c11 = rs_ok ? sC1[drow(1, v) * Rs + c1o] : 0.f;
+      const float c10 = c1[0][v], c11 = c1[1][v];
       an1[0][v] = fmaf(dz, T10[v], an1[0][v]);
       an1[1][v] = fmaf(dz, T11[v], an1[1][v]);
       as1[v] = fmaf(dv, hw == 0 ? m0 : m1, as1[v]);
-      T10[v] = dz * (i < Rn ? sN1[drow(0, v) * Rn + n1o] : 0.f);
-      T11[v] = dz * (i < Rn ? sN1[drow(1, v) * Rn + n1o] : 0.f);
+      T10[v] = dz * n1[0][v];
+      T11[v] = dz * n1[1][v];
       const float q0 = m0 > 0.f ? dv * c10 * __builtin_amdgcn_rcpf(m0) : 0.f;
       const float q1 = m1 > 0.f ? dv * c11 * __builtin_amdgcn_rcpf(m1) : 0.f;
       T00[v] = q0 * T00[v];
@@ -490,27 +516,47 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         dma_tail(nn);
       }
+      sl_f4 pa, pb;
+      if (TR_SLICE_BPF) {
+        pa = *reinterpret_cast<const sl_f4*>(slice + bo0);
+        pb = *reinterpret_cast<const sl_f4*>(slice + bo1);
+      }
 #pragma unroll
       for (int q = 0; q < SL_TILES; ++q) {
         if (q < ntl) {
-          const sl_f4 va = *reinterpret_cast<const sl_f4*>(slice + 512 * q + bo0);
-          const sl_f4 vb = *reinterpret_cast<const sl_f4*>(slice + 512 * q + bo1);
+          sl_f4 va, vb;
+          if (TR_SLICE_BPF) {
+            va = pa;
+            vb = pb;
+            if (q + 1 < ntl) {
+              pa = *reinterpret_cast<const sl_f4*>(slice + 512 * (q + 1) + bo0);
+              pb = *reinterpret_cast<const sl_f4*>(slice + 512 * (q + 1) + bo1);
+            }
+          } else {
+            va = *reinterpret_cast<const sl_f4*>(slice + 512 * q + bo0);
+            vb = *reinterpret_cast<const sl_f4*>(slice + 512 * q + bo1);
+          }
+          // the tile's two LDS-DMA pieces of the next sample go out between its MFMAs (after
+          // the reads landed), not back to back: bursts stall on the memory issue queue
 #pragma unroll
-          for (int v = 0; v < 4 && !(TR_SLICE_SKIP & 4); ++v) {
+          for (int v = 0; v < 4; ++v) {
             const sl_f4& src = v < 2 ? va : vb;
             const float a0 = src[2 * (v & 1) + 0], a1 = src[2 * (v & 1) + 1];
-            gacc[q][0] = sl_mfma(a0, T00[v], gacc[q][0]);
-            gacc[q][1] = sl_mfma(a0, T10[v], gacc[q][1]);
-            gacc[q][0] = sl_mfma(a1, T01[v], gacc[q][0]);
-            gacc[q][1] = sl_mfma(a1, T11[v], gacc[q][1]);
+            if (!(TR_SLICE_SKIP & 4)) {
+              gacc[q][0] = sl_mfma(a0, T00[v], gacc[q][0]);
+              gacc[q][1] = sl_mfma(a0, T10[v], gacc[q][1]);
+              gacc[q][0] = sl_mfma(a1, T01[v], gacc[q][0]);
+              gacc[q][1] = sl_mfma(a1, T11[v], gacc[q][1]);
+            }
+            if (has_next && (v & 1)) {
+              if (v == 1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // tile q's reads landed
+              // (with TR_SLICE_BPF the next tile's two reads may still be in flight: waited too)
+              dma_piece(nn, q, v >> 1);
+            }
           }
           if (Dt > 0 && q / TQ == p) {
             gacc[q][0] = sl_mfma(at[q % TQ], dTt0, gacc[q][0]);
             gacc[q][1] = sl_mfma(at[q % TQ], dTt1, gacc[q][1]);
-          }
-          if (has_next) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // tile q's reads have landed
-            dma_tile(nn, q);
           }
         }
       }
@@ -591,7 +637,7 @@ void spec_slice_geom(SpecGeom* g) {
   const int Dt = g->D > 128 ? g->D - 128 : 0;
   if (g->NO > 64) return;
   g->slDt = Dt;
-  g->sl_Dp = g->D > 128 ? g->D : 128;
+  g->sl_Dp = ((g->D > 128 ? g->D : 128) + 3) & ~3;
   g->sl_oTail = SL_NW * SL_SLICE;
   g->sl_oEx = g->sl_oTail + SL_NW * SL_TAIL;
   g->sl_oTP = g->sl_oEx + SL_NW * TR_WAVE * 8;

@@ -210,7 +210,7 @@ def _slice_shape(W, D, Rn, Rs, ncd, O):
     """the column-slice kernel's envelope (spec_slice_geom in csrc/tr_spectral_slice.hip)"""
     ok = (W == 256 and 97 <= D <= 130 and (D >= 128 or D % 4 == 0) and 1 <= Rn <= 16 and Rs >= 1
           and Rs * (ncd + 1) <= 16 and ncd + 1 in (1, 2, 4) and O <= 64)
-    small = max(D, 128) * (Rn + Rs) + O * 33 + 16 + O * (Rn + Rs + 1) + 64
+    small = ((max(D, 128) + 3) // 4 * 4) * (Rn + Rs) + O * 33 + 16 + O * (Rn + Rs + 1) + 64
     return ok and (38144 + ((small + 3) & ~3) + 4) * 4 <= 160 * 1024
 
 
