@@ -51,6 +51,14 @@
 #ifndef TR_SLICE_BPF
 #define TR_SLICE_BPF 1  // gradient GEMM: next tile's operand reads issued before this tile's MFMAs
 #endif
+#ifndef TR_SLICE_NT
+#define TR_SLICE_NT 1  // non-temporal policy on the slice LDS-DMA
+#endif
+#if TR_SLICE_NT
+#define SL_NT " nt"
+#else
+#define SL_NT ""
+#endif
 #ifndef TR_SLICE_PROFILE
 #define TR_SLICE_PROFILE 0  // profiling build: per-phase cycle counts of wave 0 of workgroups 0..255
 #endif
@@ -128,7 +136,7 @@ __device__ __forceinline__ uint32_t sl_lds_addr(const float* p) {
 // one 4-B LDS-DMA piece per lane: gsrc -> LDS byte address m0 + 4 * lane (m0 saved / restored)
 __device__ __forceinline__ void sl_dma4(const float* gsrc, const float* lds_dst) {
   uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off nt\n\ts_mov_b32 m0, %0"
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off" SL_NT "\n\ts_mov_b32 m0, %0"
                : "=&s"(keep)
                : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(sl_lds_addr(lds_dst)))
                : "memory");
@@ -136,7 +144,7 @@ __device__ __forceinline__ void sl_dma4(const float* gsrc, const float* lds_dst)
 // one 16-B LDS-DMA piece per lane: gsrc (4-B aligned is enough) -> LDS byte address m0 + 16 * lane
 __device__ __forceinline__ void sl_dma16(const float* gsrc, const float* lds_dst) {
   uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" SL_NT "\n\ts_mov_b32 m0, %0"
                : "=&s"(keep)
                : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(sl_lds_addr(lds_dst)))
                : "memory");
