@@ -52,7 +52,7 @@
 #define TR_SLICE_BPF 1  // gradient GEMM: next tile's operand reads issued before this tile's MFMAs
 #endif
 #ifndef TR_SLICE_NT
-#define TR_SLICE_NT 1  // non-temporal policy on the slice LDS-DMA
+#define TR_SLICE_NT 0  // non-temporal policy on the slice LDS-DMA (off: neighbour pairs share row lines in L2; nt gave 1.29x HBM traffic, default 1.05x)
 #endif
 #if TR_SLICE_NT
 #define SL_NT " nt"
