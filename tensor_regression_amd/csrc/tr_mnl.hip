@@ -268,9 +268,14 @@ __device__ __forceinline__ void mnl_body(const MnlGeom& g, const MnArgs& a, cons
   const int64_t n1 = n0 + a.rows_per_wg < a.N ? n0 + a.rows_per_wg : a.N;
   const int64_t nr = n1 > n0 ? n1 - n0 : 0;
   auto sample_of = [&](int64_t k) -> int64_t { return a.reverse ? (n1 - 1 - k) : (n0 + k); };
-  auto issue_group = [&](int64_t n, int buf, int gi) {
-    if (goff[gi] >= 0) mn_dma16(a.X + n * a.xld + goff[gi], lds + (int64_t)buf * SPF + (wv + MN_NW * gi) * 256);
+  // (the sample's base pointers are formed once per call site; FULL shapes have every piece of
+  // every group valid, so no per-lane test -- and no exec-mask branch -- around the DMA)
+  auto issue_at = [&](const float* src, float* dst, int gi) {
+    if (FULL || goff[gi] >= 0) mn_dma16(src + goff[gi], dst + MN_NW * gi * 256);
   };
+  auto dma_src = [&](int64_t n) { return a.X + n * a.xld; };
+  auto dma_dst = [&](int buf) { return lds + buf * SPF + wv * 256; };
+  auto issue_group = [&](int64_t n, int buf, int gi) { issue_at(dma_src(n), dma_dst(buf), gi); };
 
   for (int e = t; e < 4 * 16 * 4; e += MN_T) sZ[e] = 0.f;
   __syncthreads();
@@ -295,7 +300,9 @@ __device__ __forceinline__ void mnl_body(const MnlGeom& g, const MnArgs& a, cons
   // on the vector-memory issue queue)
   auto gemm1 = [&](int buf, int zidx, mn_f32x4(&acc)[4], float& u0, float& u1, float& u2, float& u3, bool dma_on,
                    int64_t dma_n, int dma_buf) {
-    const float* sb = lds + (int64_t)buf * SPF;
+    const float* sb = lds + buf * SPF;
+    const float* dsrc = dma_on ? dma_src(dma_n) : a.X;
+    float* ddst = dma_dst(dma_buf);
 #pragma unroll
     for (int q = 0; q < 4; ++q) acc[q] = mn_f32x4{0.f, 0.f, 0.f, 0.f};
     float4 xr[16];
@@ -309,7 +316,7 @@ __device__ __forceinline__ void mnl_body(const MnlGeom& g, const MnArgs& a, cons
         if (FULL || 4 * c4 < klen) xr[c4] = *reinterpret_cast<const float4*>(rp + 4 * ((16 * jb + c4) ^ sw));
 #pragma unroll
       for (int c4 = 0; c4 < 16; ++c4) {
-        if (TR_MNL_DMA_IN_GEMM && dma_on && (c4 & 1) == 0 && (c4 >> 1) < gcnt) issue_group(dma_n, dma_buf, c4 >> 1);
+        if (TR_MNL_DMA_IN_GEMM && dma_on && (c4 & 1) == 0 && (c4 >> 1) < gcnt) issue_at(dsrc, ddst, c4 >> 1);
         if (FULL || 4 * c4 < klen) {
           acc[0] = mfma_4x4(xr[c4].x, bop[4 * c4 + 0], acc[0]);
           acc[1] = mfma_4x4(xr[c4].y, bop[4 * c4 + 1], acc[1]);
@@ -348,7 +355,7 @@ __device__ __forceinline__ void mnl_body(const MnlGeom& g, const MnArgs& a, cons
       }
 #pragma unroll
       for (int st = 0; st < 16; ++st) {
-        if (TR_MNL_DMA_IN_GEMM && dma_on && (st & 1) == 0 && (st >> 1) < gcnt) issue_group(dma_n, dma_buf, st >> 1);
+        if (TR_MNL_DMA_IN_GEMM && dma_on && (st & 1) == 0 && (st >> 1) < gcnt) issue_at(dsrc, ddst, st >> 1);
         if (FULL || 4 * st < klen) {
           acc[0] = mfma_4x4(xr[st].x, bop[st], acc[0]);
           acc[1] = mfma_4x4(xr[st].y, bop[st], acc[1]);
@@ -452,20 +459,21 @@ __device__ __forceinline__ void mnl_body(const MnlGeom& g, const MnArgs& a, cons
     // ---- two samples (a pair) per barrier: ring slots 2 (p % nps) + h, member h in 16-lane
     // rows 2h, 2h+1 of the epilogue (both members' softmax chains in the same instructions) ----
     const int nps = nbuf / 2;
-    const int64_t np = (nr + 1) / 2;
+    const int np = (int)((nr + 1) / 2);  // (rows per workgroup < 2^31)
     // an odd range's last pair repeats the last sample with class weight 0 (contributes 0)
-    auto member_sample = [&](int64_t kk) -> int64_t { return sample_of(kk < nr ? kk : nr - 1); };
-    auto issue_pair = [&](int64_t p) {
-      const int s0 = 2 * (int)(p % nps);
+    auto member_sample = [&](int kk) -> int64_t { return sample_of(kk < nr ? kk : nr - 1); };
+    auto issue_pair = [&](int p, int slot) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const int64_t n = member_sample(2 * p + h);
+        const float* src = dma_src(member_sample(2 * p + h));
+        float* dst = dma_dst(2 * slot + h);
 #pragma unroll
         for (int gi = 0; gi < kMnlGMax; ++gi)
-          if (gi < gcnt) issue_group(n, s0 + h, gi);
+          if (gi < gcnt) issue_at(src, dst, gi);
       }
     };
-    for (int64_t p = 0; p < nps - 1 && p < np; ++p) issue_pair(p);
+    for (int p = 0; p < nps - 1 && p < np; ++p) issue_pair(p, p);
+    int slot_cur = 0, slot_pre = nps - 1;  // ring slots of pair p and of pair p + nps - 1 (mod nps)
     mn_f32x4 accA[4], accB[4];  // members a, b of the previous pair (GEMM output of this pair)
 #pragma unroll
     for (int q = 0; q < 4; ++q) accA[q] = accB[q] = mn_f32x4{0.f, 0.f, 0.f, 0.f};
@@ -473,20 +481,20 @@ __device__ __forceinline__ void mnl_body(const MnlGeom& g, const MnArgs& a, cons
     int64_t ya = 0, yb = 0;
     float cwa = 0.f, cwb = 0.f;
     const int h = lane >> 5;  // epilogue member of this lane
-    for (int64_t p = 0; p <= np; ++p) {
+    for (int p = 0; p <= np; ++p) {
       if (p < np) {
-        int64_t ahead = np - 1 - p;
+        int ahead = np - 1 - p;
         if (ahead > nps - 2) ahead = nps - 2;
-        mn_wait_vm(2 * gcnt * (int)ahead);  // pair p has landed (this wave's pieces)
+        mn_wait_vm(2 * gcnt * ahead);  // pair p has landed (this wave's pieces)
       }
       TR_MNL_MARK(0);
       mn_barrier();  // every wave's pieces of pair p; Z partials of p - 1; slots of pair p - 1 free
       TR_MNL_MARK(1);
       const bool pre = p + nps - 1 < np;  // refill the slots of pair p - 1 with pair p + nps - 1
       const bool pre_in_gemm = TR_MNL_DMA_IN_GEMM && ROLE != MN_ROLE_IDLE && p < np;
-      if (pre && !pre_in_gemm) issue_pair(p + nps - 1);
-      const int64_t pq = p + nps - 1;
-      const int spre = 2 * (int)(pq % nps);
+      if (pre && !pre_in_gemm) issue_pair(p + nps - 1, slot_pre);
+      const int pq = p + nps - 1;
+      const int spre = 2 * slot_pre;
       TR_MNL_MARK(2);
       if (ROLE != MN_ROLE_IDLE) {
         if (p >= 1) {
@@ -518,7 +526,7 @@ __device__ __forceinline__ void mnl_body(const MnlGeom& g, const MnArgs& a, cons
         }
         TR_MNL_MARK(3);
         if (p < np) {
-          const int s0 = 2 * (int)(p % nps), zs = (int)(p & 1);
+          const int s0 = 2 * slot_cur, zs = p & 1;
           ya = lab[member_sample(2 * p)];
           cwa = class_w[ya];
           yb = lab[member_sample(2 * p + 1)];
@@ -530,6 +538,8 @@ __device__ __forceinline__ void mnl_body(const MnlGeom& g, const MnArgs& a, cons
         }
       }
       TR_MNL_MARK(4);
+      slot_cur = slot_cur + 1 == nps ? 0 : slot_cur + 1;
+      slot_pre = slot_pre + 1 == nps ? 0 : slot_pre + 1;
     }
   }
 #if TR_MNL_PROFILE
