@@ -44,6 +44,9 @@
 #ifndef TR_MNL_DMA_IN_GEMM
 #define TR_MNL_DMA_IN_GEMM 1  // issue the ring refill between GEMM steps instead of after the barrier
 #endif
+#ifndef TR_MNL_HOIST
+#define TR_MNL_HOIST 4  // operand quads of pair member a loaded before the previous pair's epilogue
+#endif
 #ifndef TR_MNL_PROFILE
 #define TR_MNL_PROFILE 0  // profiling build only: per-phase cycle counts of every wave of WG 0..255
 #endif
@@ -199,6 +202,9 @@ __device__ __forceinline__ void mnl_body(const MnlGeom& g, const MnArgs& a, cons
   const float* PC = a.phi + g.offPC;
   const int c = lane & 15, grow = lane >> 4;
   const bool cok = c < C;
+  // class weight of class c in lane c of every 16-lane row: a label's weight is one readlane, not
+  // a second scalar load that waits on the label load (and, through lgkmcnt, on the GEMM's LDS reads)
+  const float cwl = cok ? class_w[c] : 0.f;
 
   int ib = 0, jb = 0, rb = 0;
   if (ROLE == MN_ROLE_A) {
@@ -298,14 +304,10 @@ __device__ __forceinline__ void mnl_body(const MnlGeom& g, const MnArgs& a, cons
   // dma_on: also issue this wave's LDS-DMA pieces of sample dma_n into ring slot dma_buf, one
   // piece every other k step between the MFMAs (a burst of them right after the barrier stalls
   // on the vector-memory issue queue)
-  auto gemm1 = [&](int buf, int zidx, mn_f32x4(&acc)[4], float& u0, float& u1, float& u2, float& u3, bool dma_on,
-                   int64_t dma_n, int dma_buf) {
+  // the member's X operands from ring slot `buf` into xr (issued early by the pair loop, so that
+  // their LDS latency hides under the previous pair's epilogue)
+  auto load1 = [&](int buf, float4(&xr)[16], int s0 = 0, int s1 = 16) {
     const float* sb = lds + buf * SPF;
-    const float* dsrc = dma_on ? dma_src(dma_n) : a.X;
-    float* ddst = dma_dst(dma_buf);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) acc[q] = mn_f32x4{0.f, 0.f, 0.f, 0.f};
-    float4 xr[16];
     if (ROLE == MN_ROLE_A) {
       int row = 64 * ib + lane;
       if (!FULL) row = row < I ? row : I - 1;
@@ -313,7 +315,33 @@ __device__ __forceinline__ void mnl_body(const MnlGeom& g, const MnArgs& a, cons
       const int sw = row & g.smask;
 #pragma unroll
       for (int c4 = 0; c4 < 16; ++c4)
-        if (FULL || 4 * c4 < klen) xr[c4] = *reinterpret_cast<const float4*>(rp + 4 * ((16 * jb + c4) ^ sw));
+        if (c4 >= s0 && c4 < s1 && (FULL || 4 * c4 < klen))
+          xr[c4] = *reinterpret_cast<const float4*>(rp + 4 * ((16 * jb + c4) ^ sw));
+    } else if (ROLE == MN_ROLE_B) {
+      int cq = 16 * jb + c;
+      if (!FULL) cq = cq < g.JQ ? cq : g.JQ - 1;
+#pragma unroll
+      for (int st = 0; st < 16; ++st) {
+        if (st >= s0 && st < s1 && (FULL || 4 * st < klen)) {
+          int i = 64 * ib + 4 * st + grow;
+          if (!FULL) i = i < I ? i : I - 1;
+          xr[st] = *reinterpret_cast<const float4*>(sb + i * J + 4 * (cq ^ (i & g.smask)));
+        }
+      }
+    }
+  };
+  // GEMM of the sample whose operands are in xr: A-units T (summed into acc[0]) and their Z
+  // partial -> sZ[zidx]; B-units V (acc[0..3]).  u0..u3: the A-unit's U partial (ranks 4 rb + q).
+  // dma_on: also issue this wave's LDS-DMA pieces of sample dma_n into ring slot dma_buf, one
+  // piece every other k step between the MFMAs (a burst of them right after the barrier stalls
+  // on the vector-memory issue queue)
+  auto gemm1 = [&](const float4(&xr)[16], int zidx, mn_f32x4(&acc)[4], float& u0, float& u1, float& u2, float& u3,
+                   bool dma_on, int64_t dma_n, int dma_buf) {
+    const float* dsrc = dma_on ? dma_src(dma_n) : a.X;
+    float* ddst = dma_dst(dma_buf);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] = mn_f32x4{0.f, 0.f, 0.f, 0.f};
+    if (ROLE == MN_ROLE_A) {
 #pragma unroll
       for (int c4 = 0; c4 < 16; ++c4) {
         if (TR_MNL_DMA_IN_GEMM && dma_on && (c4 & 1) == 0 && (c4 >> 1) < gcnt) issue_at(dsrc, ddst, c4 >> 1);
@@ -343,16 +371,6 @@ __device__ __forceinline__ void mnl_body(const MnlGeom& g, const MnArgs& a, cons
       zpart = fmaf(wpc[3], u3, zpart);
       if (lane < 16) sZ[(zidx * 16 + lane) * 4 + wv] = zpart;
     } else {
-      int cq = 16 * jb + c;
-      if (!FULL) cq = cq < g.JQ ? cq : g.JQ - 1;
-#pragma unroll
-      for (int st = 0; st < 16; ++st) {
-        if (FULL || 4 * st < klen) {
-          int i = 64 * ib + 4 * st + grow;
-          if (!FULL) i = i < I ? i : I - 1;
-          xr[st] = *reinterpret_cast<const float4*>(sb + i * J + 4 * (cq ^ (i & g.smask)));
-        }
-      }
 #pragma unroll
       for (int st = 0; st < 16; ++st) {
         if (TR_MNL_DMA_IN_GEMM && dma_on && (st & 1) == 0 && (st >> 1) < gcnt) issue_at(dsrc, ddst, st >> 1);
@@ -441,8 +459,10 @@ __device__ __forceinline__ void mnl_body(const MnlGeom& g, const MnArgs& a, cons
         }
         if (k < nr) {
           yC = lab[sample_of(k)];
-          cwC = class_w[yC];
-          gemm1((int)(k % nbuf), (int)(k & 1), accC, uC0, uC1, uC2, uC3, pre, npre, bpre);
+          cwC = rdl(cwl, (int)yC);
+          float4 xr[16];
+          load1((int)(k % nbuf), xr);
+          gemm1(xr, (int)(k & 1), accC, uC0, uC1, uC2, uC3, pre, npre, bpre);
 #pragma unroll
           for (int q = 0; q < 4; ++q) accP[q] = accC[q];
           uP0 = uC0;
@@ -496,6 +516,9 @@ __device__ __forceinline__ void mnl_body(const MnlGeom& g, const MnArgs& a, cons
       const int pq = p + nps - 1;
       const int spre = 2 * slot_pre;
       TR_MNL_MARK(2);
+      float4 xra[16];  // member a's first TR_MNL_HOIST operand quads, in flight across the epilogue
+      constexpr int HO = FULL ? TR_MNL_HOIST : 0;
+      if (HO > 0 && ROLE != MN_ROLE_IDLE && p < np) load1(2 * slot_cur, xra, 0, HO);
       if (ROLE != MN_ROLE_IDLE) {
         if (p >= 1) {
           const int zs = (int)((p - 1) & 1);
@@ -528,12 +551,14 @@ __device__ __forceinline__ void mnl_body(const MnlGeom& g, const MnArgs& a, cons
         if (p < np) {
           const int s0 = 2 * slot_cur, zs = p & 1;
           ya = lab[member_sample(2 * p)];
-          cwa = class_w[ya];
+          cwa = rdl(cwl, (int)ya);
           yb = lab[member_sample(2 * p + 1)];
-          cwb = 2 * p + 1 < nr ? class_w[yb] : 0.f;
-          gemm1(s0, zs * 2, accA, ua0, ua1, ua2, ua3, pre, pre ? member_sample(2 * pq) : 0, spre);
+          cwb = 2 * p + 1 < nr ? rdl(cwl, (int)yb) : 0.f;
+          load1(s0, xra, HO, 16);
+          gemm1(xra, zs * 2, accA, ua0, ua1, ua2, ua3, pre, pre ? member_sample(2 * pq) : 0, spre);
           TR_MNL_MARK(5);
-          gemm1(s0 + 1, zs * 2 + 1, accB, ub0, ub1, ub2, ub3, pre, pre ? member_sample(2 * pq + 1) : 0, spre + 1);
+          load1(s0 + 1, xra);
+          gemm1(xra, zs * 2 + 1, accB, ub0, ub1, ub2, ub3, pre, pre ? member_sample(2 * pq + 1) : 0, spre + 1);
           TR_MNL_MARK(6);
         }
       }
