@@ -179,10 +179,11 @@ class Plan:
             self.h = None
             self.lib.tr_plan_destroy(h)
 
-    def __del__(self):
+    def __del__(self, _is_finalizing=sys.is_finalizing):
         # during interpreter shutdown the exit hook has already destroyed every plan; never call
-        # into HIP from a finaliser that may run after the runtime is gone
-        if sys.is_finalizing():
+        # into HIP from a finaliser that may run after the runtime is gone (the default argument
+        # keeps the function reachable after module globals such as `sys` have been cleared)
+        if _is_finalizing():
             return
         try:
             self.destroy()
