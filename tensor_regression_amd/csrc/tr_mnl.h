@@ -37,6 +37,10 @@ struct MnlGeom {
   int64_t offP1, offPC, nfelem, slab;  // arena offsets (floats); slab stride (nfelem rounded to 4)
   // LDS carve (floats)
   int oZ, oG, lds_floats;  // oZ: [2][2][16][4] Z partials; oG: LDS image of the arena (aliases the drained ring)
+  // two-workgroups-per-CU variant (tr_mnl_duo.hip): 4 waves, each owning every rank block of
+  // one (i, j) block; LDS carve of ONE workgroup (floats)
+  int duo;
+  int du_oZ, du_oP1, du_oG, du_lds_floats;
 };
 
 // Fills g; false (with a reason) when the shape is outside the kernel's envelope.
@@ -49,5 +53,15 @@ hipError_t mnl_prepare(const MnlGeom& g, int* ok);
 hipError_t launch_mnl_fused(const MnlGeom& g, int grid, const float* X, int64_t N, int64_t xld, const float* phi,
                             const float* w, const int64_t* lab, const float* class_w, float scale, float* gpart,
                             double* dpart, int64_t rows_per_wg, int reverse, const int32_t* stop, hipStream_t st);
+
+// Two-workgroups-per-CU variant (tr_mnl_duo.hip): sets g->duo when the shape fits it (two 64-row
+// blocks, R <= 8, LDS for two workgroups; TR_MNL_DUO=0 turns it off), then checks the compiled
+// kernel is spill-free and two of its workgroups fit a CU.
+void mnl_duo_geom(MnlGeom* g);
+hipError_t mnl_duo_prepare(MnlGeom* g);
+// Same contract as launch_mnl_fused, with grid = 2 workgroups per CU.
+hipError_t launch_mnl_duo(const MnlGeom& g, int grid, const float* X, int64_t N, int64_t xld, const float* phi,
+                          const float* w, const int64_t* lab, const float* class_w, float scale, float* gpart,
+                          double* dpart, int64_t rows_per_wg, int reverse, const int32_t* stop, hipStream_t st);
 
 }  // namespace tr

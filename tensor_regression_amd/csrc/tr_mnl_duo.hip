@@ -1,0 +1,521 @@
+// tr_mnl_duo.hip — the factored multinomial single pass as TWO workgroups per CU (BASELINE
+// config 3: X (65536, 128, 64), 10 classes, rank 8; multinomial_tensor_regression.py model
+// :148-187, CrossEntropyLoss of fit_Adam :448-457, autograd :457).
+//
+// Same math and unit decomposition as k_mnl_fused (tr_mnl.hip header): per sample
+//     T[i, r] = sum_j X_n[i, j] Phi1[j, r]   (A-units)     V[j, r] = sum_i X_n[i, j] Phi0[i, r]  (B-units)
+//     U -> Z -> softmax, CE on the probabilities, dZ -> Wv -> dPhi0 += Wv T, dPhi1 += Wv V, dPhiC
+// on v_mfma_f32_4x4x1_16b_f32.  k_mnl_fused runs ONE 8-wave workgroup per CU over a 4-sample LDS
+// ring: every wave waits at one barrier per pair, and between barriers each wave does its GEMM
+// unit and the softmax epilogue back to back, so the matrix pipe is busy ~22 % and the
+// kernel is latency-bound.  Here a workgroup is 4 waves (2 A-waves, 2 B-waves, each
+// wave owning BOTH rank blocks of its (i, j) block: one set of X operand reads feeds two units)
+// over a 2-sample ring (2 x 32 KiB), and TWO workgroups share a CU: while one workgroup sits in
+// its barrier or its latency-bound epilogue, the other's MFMAs run on the same SIMDs.
+//
+// Per sample k of a workgroup: wait own LDS-DMA of k -> barrier -> epilogue of k-1 (Z partials
+// of the 2 A-waves, double softmax, Wv, gradient scaling) -> GEMM of k with the DMA of k+1 into
+// the other ring slot interleaved.  The A-waves read Phi1 (their B operand) from a transposed
+// LDS table instead of 128 resident registers.  Numerics: the unit arithmetic, the Z partial
+// slots, the summation orders and the slab accumulation order are those of k_mnl_fused.
+#include <cstdlib>
+#include <cstring>
+
+#include "tr_common.h"
+#include "tr_mnl.h"
+
+#ifndef TR_DUO_SKIP
+#define TR_DUO_SKIP 0  // profiling ablation only (results invalid): 1 loop LDS-DMA, 2 MFMAs, 4 epilogue
+#endif
+
+namespace tr {
+
+namespace {
+constexpr int DU_NW = 4;
+constexpr int DU_T = DU_NW * TR_WAVE;
+#ifndef TR_DUO_XL
+#define TR_DUO_XL 8
+#endif
+constexpr int XL = TR_DUO_XL;  // GEMM steps an operand quad is read ahead of its MFMAs
+constexpr int DU_GMAX = 12;  // LDS-DMA pieces (1 KiB) per wave per sample (sample <= 48 KiB)
+typedef float du_f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ du_f32x4 du_mfma(float a, float b, du_f32x4 c) {
+  if (TR_DUO_SKIP & 2) return c + a * b;  // one VALU op instead of the MFMA (keeps the operand reads)
+  return __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, c, 0, 0, 0);
+}
+template <int CTRL>
+__device__ __forceinline__ float du_dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float du_row_sum16(float v) {
+  v += du_dpp<0xB1>(v);
+  v += du_dpp<0x4E>(v);
+  v += du_dpp<0x141>(v);
+  v += du_dpp<0x140>(v);
+  return v;
+}
+__device__ __forceinline__ float du_row_max16(float v) {
+  v = fmaxf(v, du_dpp<0xB1>(v));
+  v = fmaxf(v, du_dpp<0x4E>(v));
+  v = fmaxf(v, du_dpp<0x141>(v));
+  v = fmaxf(v, du_dpp<0x140>(v));
+  return v;
+}
+__device__ __forceinline__ float du_xor16_sum(float v) {
+  const auto q = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(q[0]) + __uint_as_float(q[1]);
+}
+__device__ __forceinline__ float du_xor32_sum(float v) {
+  const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(q[0]) + __uint_as_float(q[1]);
+}
+// exp / log on the hardware base-2 units (v_exp_f32 / v_log_f32, ~1 ulp): the epilogue's
+// arguments are bounded (exp of values <= 0 and of S in [0, 1], log of a sum in [1, 16 e])
+__device__ __forceinline__ float du_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
+__device__ __forceinline__ float du_log(float x) { return __builtin_amdgcn_logf(x) * 0.6931471805599453f; }
+__device__ __forceinline__ float du_rdl(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ void du_barrier() {  // leaves LDS-DMA in flight
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ void du_dma16(const float* gsrc, const float* lds_dst) {
+  const uint32_t a = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) float*)lds_dst);
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(a))
+               : "memory");
+}
+}  // namespace
+
+struct DuArgs {
+  const float* X;
+  int64_t N, xld;
+  const float* phi;
+  const float* w;
+  float scale;
+  float* gpart;
+  double* dpart;
+  int64_t rows_per_wg;
+  int reverse;
+};
+
+// ROLE 0: A-wave (i block, j block) -> T for both rank blocks; ROLE 1: B-wave -> V
+template <int ROLE, int NRB>
+__device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, const int64_t* __restrict__ lab,
+                                         const float* __restrict__ class_w, float* lds, const int wv, const int lane) {
+  const int t = threadIdx.x;
+  const int I = g.I, J = g.J, R = g.R, C = g.C;
+  constexpr int nrb = NRB;  // rank blocks of 4 (1 or 2)
+  const int SPF = I * J;
+  float* sZ = lds + g.du_oZ;    // [2 parity][16 classes][4 A-unit slots]
+  float* sP1 = lds + g.du_oP1;  // Phi1^T [R][J + 4] (A-waves' B operand, 4 consecutive k per b128)
+  const int P1S = J + 4;
+  const float* P0 = a.phi;
+  const float* P1 = a.phi + g.offP1;
+  const float* PC = a.phi + g.offPC;
+  const int c = lane & 15, grow = lane >> 4, l3 = lane & 3;
+  const bool cok = c < C;
+  const float cwl = cok ? class_w[c] : 0.f;  // class weight of class c in lane c of every row
+  const float NEG = -__builtin_huge_valf();
+  float sel[4];  // 1 where l & 3 == q
+#pragma unroll
+  for (int q = 0; q < 4; ++q) sel[q] = l3 == q ? 1.f : 0.f;
+
+  // (i, j) block of this wave: A-units of k_mnl_fused number rb + nrb * (jb + njb * ib), B-units
+  // rb + nrb * (ib + nib * jb); a wave here is one (ib, jb) set with every rank block
+  const int s = ROLE == 0 ? wv : wv - 2;
+  const int ib = ROLE == 0 ? s / g.njb : s % g.nib;
+  const int jb = ROLE == 0 ? s % g.njb : s / g.nib;
+
+  // per rank block rb: rank of this lane's accumulator column, factor registers
+  float phiU[2][4], wpc[2][4], pcg[2], wg[2];
+  float bopB[2][16];  // B-waves: Phi0[64 ib + 4 st + grow][rq]
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb) {
+    const int rq = 4 * rb + l3;
+    const bool ok = rb < nrb && rq < R;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int row = 64 * ib + 4 * (lane >> 2) + v;
+      phiU[rb][v] = (ROLE == 0 && ok) ? P0[(int64_t)row * R + rq] : 0.f;
+      const int r = 4 * rb + v;
+      wpc[rb][v] = (ROLE == 0 && rb < nrb && cok && r < R) ? a.w[r] * PC[c * R + r] : 0.f;
+    }
+    const int r = 4 * rb + grow;
+    pcg[rb] = (rb < nrb && cok && r < R) ? a.w[r] * PC[c * R + r] : 0.f;
+    wg[rb] = (rb < nrb && r < R) ? a.w[r] : 0.f;
+#pragma unroll
+    for (int st = 0; st < 16; ++st)
+      bopB[rb][st] = (ROLE == 1 && ok) ? P0[(int64_t)(64 * ib + 4 * st + grow) * R + rq] : 0.f;
+  }
+  // Phi1^T table (A-waves' B operands), rank rows padded to 4 nrb with zeros (a padded rank's
+  // T column must stay finite: U sums every lane's column times phiU, which is 0 there)
+  for (int e = t; e < 4 * nrb * J; e += DU_T) {
+    const int r = e / J, j = e - r * J;
+    sP1[r * P1S + j] = r < R ? P1[(int64_t)j * R + r] : 0.f;
+  }
+  for (int e = t; e < 2 * 16 * 4; e += DU_T) sZ[e] = 0.f;
+
+  // LDS-DMA map: wave wv issues the 1 KiB groups wv + 4 gi of every sample
+  const int ngroups = g.nchunk / TR_WAVE;  // (full shapes: nchunk % 64 == 0)
+  const int gcnt = ngroups > wv ? (ngroups - wv + DU_NW - 1) / DU_NW : 0;
+  int goff[DU_GMAX];
+#pragma unroll
+  for (int gi = 0; gi < DU_GMAX; ++gi) {
+    const int slot = (wv + DU_NW * gi) * TR_WAVE + lane;
+    const int i = slot / g.JQ;
+    const int q = slot - i * g.JQ;
+    goff[gi] = gi < gcnt ? i * J + 4 * (q ^ (i & g.smask)) : 0;
+  }
+  const int64_t n0 = (int64_t)blockIdx.x * a.rows_per_wg;
+  const int64_t n1 = n0 + a.rows_per_wg < a.N ? n0 + a.rows_per_wg : a.N;
+  const int nr = (int)(n1 > n0 ? n1 - n0 : 0);
+  auto sample_of = [&](int k) -> int64_t { return a.reverse ? (n1 - 1 - k) : (n0 + k); };
+  auto issue = [&](const float* src, float* dst, int gi) {
+    if (gi < gcnt) du_dma16(src + goff[gi], dst + DU_NW * gi * 256);
+  };
+  auto dst_of = [&](int buf) { return lds + buf * SPF + wv * 256; };
+
+  __syncthreads();
+  __builtin_amdgcn_s_waitcnt(0);  // retire the prologue's loads (the loop waits are counted)
+
+  du_f32x4 gacc[2][4];  // A: gacc[rb][0] (dPhi0 rows x ranks); B: all four (dPhi1 by row class)
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) gacc[rb][q] = du_f32x4{0.f, 0.f, 0.f, 0.f};
+  float dpc[2] = {0.f, 0.f};  // A: dPhiC[c][4 rb + grow]
+  double lsum = 0.0;
+
+  du_f32x4 accP[2][4];  // previous sample's GEMM output (A: accP[rb][0] = T; B: V by row class)
+  float uP[2][4];
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      accP[rb][q] = du_f32x4{0.f, 0.f, 0.f, 0.f};
+      uP[rb][q] = 0.f;
+    }
+  }
+  int64_t yP = 0;
+  float cwP = 0.f;
+
+  // ---- epilogue of one sample, in 8 stages (the chain of dependent steps is cut so that the
+  // stages can sit between the next sample's GEMM steps: its latency hides under MFMAs) ----
+  // S = softmax(Z) (multinomial…py:187), Q = softmax(S), CE = log sum exp(S) - S_y (S lies in
+  // [0, 1]: the second softmax needs no max shift), dS = (Q - e_y) cw_y / W, dZ = S (dS - <dS, S>),
+  // Wv[r] = sum_c dZ[c] w_r PhiC[c, r].  Every sum over the 16 classes that the chain needs after
+  // S is formed at once (independent DPP row sums, so their latencies overlap):
+  //   s2 = sum q, d1 = sum S q, e1 = S_y, a_r = sum S q p_r, b_r = sum S p_r, y_r = S_y p_{y,r}
+  // with q = exp(S), p_r = w_r PhiC[., r]; then <dS, S> = k (d1 / s2 - e1) and
+  // Wv[r] = k (a_r / s2 - y_r) - <dS, S> b_r  (k = cw_y / W).
+  float4 e_zp = make_float4(0.f, 0.f, 0.f, 0.f);
+  float e_x = 0.f, e_ez = 0.f, e_sum = 0.f, e_S = 0.f, e_q = 0.f, e_Sq = 0.f, e_Sy = 0.f;
+  float e_s2 = 0.f, e_d1 = 0.f, e_e1 = 0.f, e_dz = 0.f;
+  float e_ar[NRB], e_br[NRB], e_yr[NRB], e_wr[NRB], e_wv[NRB];
+  bool e_isy = false;
+  // epilogue stage st of the sample with Z partials in parity slot zs, label yE, class weight cwE
+  // (for the first call of a workgroup: zero partials, zero accumulators, cwE = 0 -> adds 0)
+  auto epi = [&](int st, int zs, int64_t yE, float cwE) {
+    if (TR_DUO_SKIP & 4) return;
+    if (st == 0) {
+      e_zp = *reinterpret_cast<const float4*>(sZ + (zs * 16 + c) * 4);
+    } else if (st == 1) {
+      const float zz = cok ? ((e_zp.x + e_zp.y) + e_zp.z) + e_zp.w : NEG;
+      e_x = zz - du_row_max16(zz);
+    } else if (st == 2) {
+      e_ez = cok ? du_exp(e_x) : 0.f;
+      e_sum = du_row_sum16(e_ez);
+    } else if (st == 3) {
+      e_S = e_ez * __builtin_amdgcn_rcpf(e_sum);
+      e_q = cok ? du_exp(e_S) : 0.f;
+      e_isy = cok && (int64_t)c == yE;
+      e_Sq = e_S * e_q;
+      e_Sy = e_isy ? e_S : 0.f;
+    } else if (st == 4) {
+      e_s2 = du_row_sum16(e_q);
+      e_d1 = du_row_sum16(e_Sq);
+      e_e1 = du_row_sum16(e_Sy);
+#pragma unroll
+      for (int rb = 0; rb < NRB; ++rb) {
+        e_ar[rb] = du_row_sum16(e_Sq * pcg[rb]);
+        e_br[rb] = du_row_sum16(e_S * pcg[rb]);
+        e_yr[rb] = du_row_sum16(e_Sy * pcg[rb]);
+      }
+    } else if (st == 5) {
+      const float is2 = __builtin_amdgcn_rcpf(e_s2);
+      const float kk = cwE * a.scale;
+      const float dot = kk * (e_d1 * is2 - e_e1);
+      if (ROLE == 0) lsum += (wv == 0 && lane == 0) ? (double)cwE * (double)(du_log(e_s2) - e_e1) : 0.0;
+      const float dS = cok ? kk * (e_q * is2 - (e_isy ? 1.0f : 0.0f)) : 0.f;
+      e_dz = cok ? e_S * (dS - dot) : 0.f;
+#pragma unroll
+      for (int rb = 0; rb < NRB; ++rb) e_wr[rb] = kk * (e_ar[rb] * is2 - e_yr[rb]) - dot * e_br[rb];
+    } else if (st == 6) {
+      // Wv[4 rb + g] in DPP row g -> lane rank 4 rb + (l & 3) by 0/1 lane masks (no branches)
+#pragma unroll
+      for (int rb = 0; rb < NRB; ++rb) {
+        const float w0 = du_rdl(e_wr[rb], 0), w1 = du_rdl(e_wr[rb], 16), w2 = du_rdl(e_wr[rb], 32),
+                    w3 = du_rdl(e_wr[rb], 48);
+        e_wv[rb] = fmaf(w3, sel[3], fmaf(w2, sel[2], fmaf(w1, sel[1], w0 * sel[0])));
+      }
+    } else {
+#pragma unroll
+      for (int rb = 0; rb < NRB; ++rb) {
+        if (ROLE == 0) {
+          gacc[rb][0] += e_wv[rb] * accP[rb][0];
+          const float ug = grow == 0 ? uP[rb][0] : grow == 1 ? uP[rb][1] : grow == 2 ? uP[rb][2] : uP[rb][3];
+          dpc[rb] = fmaf(e_dz, wg[rb] * ug, dpc[rb]);
+        } else {
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) gacc[rb][qq] += e_wv[rb] * accP[rb][qq];
+        }
+      }
+    }
+  };
+
+  if (nr > 0) {
+    const float* src = a.X + sample_of(0) * a.xld;
+#pragma unroll
+    for (int gi = 0; gi < DU_GMAX; ++gi) issue(src, dst_of(0), gi);
+  }
+  // iteration k: barrier -> GEMM of sample k with the epilogue of k - 1 between its steps and
+  // the LDS-DMA of k + 1 into the other ring slot; the epilogue of the last sample after the loop
+  for (int k = 0; k < nr; ++k) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // own pieces of sample k
+    du_barrier();  // everyone's pieces of k; Z partials of k - 1; slot (k + 1) & 1 free
+    const bool pre = k + 1 < nr && !(TR_DUO_SKIP & 1);
+    const float* psrc = pre ? a.X + sample_of(k + 1) * a.xld : a.X;
+    float* pdst = dst_of((k + 1) & 1);
+    const int zs = (k - 1) & 1;
+    const int64_t yC = lab[sample_of(k)];
+    const float cwC = du_rdl(cwl, (int)yC);
+    epi(0, zs, yP, cwP);
+    const float* sb = lds + (k & 1) * SPF;
+    du_f32x4 acc[2][4];
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[rb][q] = du_f32x4{0.f, 0.f, 0.f, 0.f};
+    if (ROLE == 0) {
+      const int row = 64 * ib + lane;
+      const float* rp = sb + row * J;
+      const int sw = row & g.smask;
+      const float* bp0 = sP1 + (0 + l3) * P1S + 64 * jb;
+      const float* bp1 = sP1 + ((nrb > 1 ? 4 : 0) + l3) * P1S + 64 * jb;
+      float4 xr[16];  // operand quads read XL steps ahead (bounded live registers)
+      auto ldA = [&](int c4) { xr[c4] = *reinterpret_cast<const float4*>(rp + 4 * ((16 * jb + c4) ^ sw)); };
+#pragma unroll
+      for (int c4 = 0; c4 < XL; ++c4) ldA(c4);
+#pragma unroll
+      for (int c4 = 0; c4 < 16; ++c4) {
+        if (c4 + XL < 16) ldA(c4 + XL);
+        if ((c4 & 1) == 0 && pre) issue(psrc, pdst, c4 >> 1);
+        const float4 b0 = *reinterpret_cast<const float4*>(bp0 + 4 * c4);
+        acc[0][0] = du_mfma(xr[c4].x, b0.x, acc[0][0]);
+        acc[0][1] = du_mfma(xr[c4].y, b0.y, acc[0][1]);
+        acc[0][2] = du_mfma(xr[c4].z, b0.z, acc[0][2]);
+        acc[0][3] = du_mfma(xr[c4].w, b0.w, acc[0][3]);
+        if (nrb > 1) {
+          const float4 b1 = *reinterpret_cast<const float4*>(bp1 + 4 * c4);
+          acc[1][0] = du_mfma(xr[c4].x, b1.x, acc[1][0]);
+          acc[1][1] = du_mfma(xr[c4].y, b1.y, acc[1][1]);
+          acc[1][2] = du_mfma(xr[c4].z, b1.z, acc[1][2]);
+          acc[1][3] = du_mfma(xr[c4].w, b1.w, acc[1][3]);
+        }
+        if ((c4 & 1) == 1 && c4 < 15) epi(1 + (c4 >> 1), zs, yP, cwP);
+      }
+      if (pre)
+#pragma unroll
+        for (int gi = 8; gi < DU_GMAX; ++gi) issue(psrc, pdst, gi);
+#pragma unroll
+      for (int rb = 0; rb < nrb; ++rb) {
+        const du_f32x4 T = (acc[rb][0] + acc[rb][1]) + (acc[rb][2] + acc[rb][3]);
+        accP[rb][0] = T;
+        float u = phiU[rb][0] * T.x;
+        u = fmaf(phiU[rb][1], T.y, u);
+        u = fmaf(phiU[rb][2], T.z, u);
+        u = fmaf(phiU[rb][3], T.w, u);
+        u += du_dpp<0x124>(u);  // row_ror:4
+        u += du_dpp<0x128>(u);  // row_ror:8
+        u = du_xor16_sum(u);
+        u = du_xor32_sum(u);
+        uP[rb][0] = du_rdl(u, 0);
+        uP[rb][1] = du_rdl(u, 1);
+        uP[rb][2] = du_rdl(u, 2);
+        uP[rb][3] = du_rdl(u, 3);
+        float zpart = wpc[rb][0] * uP[rb][0];
+        zpart = fmaf(wpc[rb][1], uP[rb][1], zpart);
+        zpart = fmaf(wpc[rb][2], uP[rb][2], zpart);
+        zpart = fmaf(wpc[rb][3], uP[rb][3], zpart);
+        if (lane < 16) sZ[((k & 1) * 16 + lane) * 4 + rb + nrb * s] = zpart;
+      }
+    } else {
+      const int cq = 16 * jb + c;
+      float4 xr[16];  // operand quads read XL steps ahead (bounded live registers)
+      auto ldB = [&](int st) {
+        const int i = 64 * ib + 4 * st + grow;
+        xr[st] = *reinterpret_cast<const float4*>(sb + i * J + 4 * (cq ^ (i & g.smask)));
+      };
+#pragma unroll
+      for (int st = 0; st < XL; ++st) ldB(st);
+#pragma unroll
+      for (int st = 0; st < 16; ++st) {
+        if (st + XL < 16) ldB(st + XL);
+        if ((st & 1) == 0 && pre) issue(psrc, pdst, st >> 1);
+#pragma unroll
+        for (int rb = 0; rb < nrb; ++rb) {
+          acc[rb][0] = du_mfma(xr[st].x, bopB[rb][st], acc[rb][0]);
+          acc[rb][1] = du_mfma(xr[st].y, bopB[rb][st], acc[rb][1]);
+          acc[rb][2] = du_mfma(xr[st].z, bopB[rb][st], acc[rb][2]);
+          acc[rb][3] = du_mfma(xr[st].w, bopB[rb][st], acc[rb][3]);
+        }
+        if ((st & 1) == 1 && st < 15) epi(1 + (st >> 1), zs, yP, cwP);
+      }
+      if (pre)
+#pragma unroll
+        for (int gi = 8; gi < DU_GMAX; ++gi) issue(psrc, pdst, gi);
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) accP[rb][q] = acc[rb][q];
+    }
+    yP = yC;
+    cwP = cwC;
+  }
+  du_barrier();  // Z partials of the last sample
+  if (nr > 0) {
+#pragma unroll
+    for (int st = 0; st < 8; ++st) epi(st, (nr - 1) & 1, yP, cwP);
+  }
+
+  // ---- fixed-order reduction into an LDS image of the arena (k_mnl_fused's unit order), slab ----
+  if (ROLE == 1) {  // fold the four row classes (lanes l, l^16, l^32, l^48)
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          float x = gacc[rb][q][v];
+          x += __shfl_xor(x, 16, TR_WAVE);
+          x += __shfl_xor(x, 32, TR_WAVE);
+          gacc[rb][q][v] = x;
+        }
+  }
+  float* sG = lds + g.du_oG;
+  __syncthreads();
+  for (int64_t e = t; e < g.slab; e += DU_T) sG[e] = 0.f;
+  __syncthreads();
+  // unit order of k_mnl_fused: A-units by (ib, jb, rb), then B-units by (jb, ib, rb)
+  for (int ws = 0; ws < DU_NW; ++ws) {
+    if (ws == wv) {
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) {
+        if (rb >= nrb) continue;
+        const int rq = 4 * rb + l3;
+        const bool rqv = rq < R;
+        if (ROLE == 0) {
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            const int row = 64 * ib + 4 * (lane >> 2) + v;
+            if (row < I && rqv) sG[row * R + rq] += gacc[rb][0][v];
+          }
+          const int r = 4 * rb + grow;
+          if (cok && r < R) sG[g.offPC + c * R + r] += dpc[rb];
+        } else if (lane < 16 && rqv) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+              const int j = 64 * jb + 16 * (lane >> 2) + 4 * v + q;
+              if (j < J) sG[g.offP1 + j * R + rq] += gacc[rb][q][v];
+            }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (ROLE == 0 && wv == 0) {
+    lsum = tr_wave_allreduce_d(lsum);
+    if (lane == 0) {
+      a.dpart[2 * blockIdx.x] = lsum;
+      a.dpart[2 * blockIdx.x + 1] = 0.0;
+    }
+  }
+  float* slab = a.gpart + (int64_t)blockIdx.x * g.slab;
+  for (int64_t e = t; e < g.slab; e += DU_T) slab[e] = sG[e];
+}
+
+template <int NRB>
+__global__ __launch_bounds__(DU_T, 2) void k_mnl_duo(MnlGeom g, DuArgs a, const int64_t* __restrict__ lab,
+                                                  const float* __restrict__ class_w, const int32_t* __restrict__ stop) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  if (stop != nullptr && *stop != 0) return;
+  const int lane = threadIdx.x & (TR_WAVE - 1);
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / TR_WAVE);
+  if (wv < 2)
+    duo_body<0, NRB>(g, a, lab, class_w, lds, wv, lane);
+  else
+    duo_body<1, NRB>(g, a, lab, class_w, lds, wv, lane);
+}
+
+// ------------------------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------------------------
+void mnl_duo_geom(MnlGeom* g) {
+  g->duo = 0;
+  const char* env = std::getenv("TR_MNL_DUO");
+  if (env != nullptr && env[0] == '0') return;
+  if (!g->full || g->nib * g->njb != 2 || g->nrb > 2 || g->C > kMnlCMax) return;
+  if (g->nchunk % TR_WAVE != 0 || g->nchunk / TR_WAVE > DU_NW * DU_GMAX) return;
+  const int64_t spf = (int64_t)g->I * g->J;
+  int64_t o = 2 * spf;  // ring of two samples
+  g->du_oZ = (int)o;
+  o += 2 * 16 * 4;
+  g->du_oP1 = (int)o;
+  o += (int64_t)g->Rp * (g->J + 4);
+  o = (o + 3) & ~(int64_t)3;
+  g->du_oG = g->slab <= 2 * spf ? 0 : (int)o;  // the arena image aliases the drained ring
+  if (g->du_oG) o += g->slab;
+  o = (o + 3) & ~(int64_t)3;
+  if (2 * o * 4 > 160 * 1024) return;  // two workgroups per CU
+  g->du_lds_floats = (int)o;
+  g->duo = 1;
+}
+
+hipError_t mnl_duo_prepare(MnlGeom* g) {
+  if (!g->duo) return hipSuccess;
+  const void* k = g->nrb == 2 ? reinterpret_cast<const void*>(&k_mnl_duo<2>) : reinterpret_cast<const void*>(&k_mnl_duo<1>);
+  const size_t lds = (size_t)g->du_lds_floats * 4;
+  hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  hipFuncAttributes attr;
+  e = hipFuncGetAttributes(&attr, k);
+  if (e != hipSuccess) return e;
+  int nb = 0;
+  e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, DU_T, lds);
+  if (e != hipSuccess) return e;
+  if (attr.localSizeBytes > 0 || nb < 2) g->duo = 0;  // spills or not two per CU: k_mnl_fused
+  return hipSuccess;
+}
+
+hipError_t launch_mnl_duo(const MnlGeom& g, int grid, const float* X, int64_t N, int64_t xld, const float* phi,
+                          const float* w, const int64_t* lab, const float* class_w, float scale, float* gpart,
+                          double* dpart, int64_t rows_per_wg, int reverse, const int32_t* stop, hipStream_t st) {
+  if (grid < 1 || rows_per_wg < 0 || xld % 4 != 0 || (int64_t)grid * rows_per_wg < N) return hipErrorInvalidValue;
+  DuArgs a{X, N, xld, phi, w, scale, gpart, dpart, rows_per_wg, reverse};
+  const size_t lds = (size_t)g.du_lds_floats * 4;
+  if (g.nrb == 2)
+    hipLaunchKernelGGL(k_mnl_duo<2>, dim3(grid), dim3(DU_T), lds, st, g, a, lab, class_w, stop);
+  else
+    hipLaunchKernelGGL(k_mnl_duo<1>, dim3(grid), dim3(DU_T), lds, st, g, a, lab, class_w, stop);
+  return hipGetLastError();
+}
+
+}  // namespace tr

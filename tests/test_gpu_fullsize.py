@@ -108,9 +108,13 @@ def test_linear_full_size_vs_fp64(cfg):
     assert errs["bias"] <= 1e-5, errs  # a sum of signed residuals (measured <= 1e-6)
 
 
-def test_multinomial_full_size_vs_fp64():
-    """Config 3: X (65536, 128, 64), 10 classes, rank 8 (the factored single pass)."""
+@pytest.mark.parametrize("duo", [True, False])
+def test_multinomial_full_size_vs_fp64(duo, monkeypatch):
+    """Config 3: X (65536, 128, 64), 10 classes, rank 8 (the factored single pass: two 4-wave
+    workgroups per CU, and with TR_MNL_DUO=0 one 8-wave workgroup per CU)."""
     from tensor_regression_amd import CP_logistic_regression
+    if not duo:
+        monkeypatch.setenv("TR_MNL_DUO", "0")
     N, I, J, C, R = 65536, 128, 64, 10, 8
     gen = torch.Generator(device=DEV).manual_seed(1234)
     X = torch.randn((N, I, J), device=DEV, generator=gen)
@@ -126,6 +130,7 @@ def test_multinomial_full_size_vs_fp64():
     dev, Xd, yd = mm._device_data()
     plan = mm._get_plan(Xd, N)
     assert "mnl-fused-1pass" in plan.describe
+    assert (" duo " in plan.describe) == duo, plan.describe
     cw = np.ones(C, np.float32)
     cwd, W = mm._class_weights(cw, dev, yd)
     arena = plan.pack(mm.Bcp)

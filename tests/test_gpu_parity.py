@@ -34,9 +34,10 @@ def path(kind):
     """kind: 'auto' (plan's choice: single pass / MFMA forward where eligible), 'twopass'
     (force the two-pass kernels: linear rows/cols, multinomial MFMA forward + cols), 'valu'
     (multinomial: two-pass with the VALU forward) or 'spi1' (multinomial single pass with one
-    sample per barrier instead of pairs)."""
+    sample per barrier instead of pairs) or 'noduo' (multinomial single pass with one 8-wave
+    workgroup per CU instead of the two-workgroups-per-CU variant)."""
     from tensor_regression_amd import standard_tensor_regression as S
-    saved = {k: os.environ.get(k) for k in ("TR_FORCE_TWOPASS", "TR_NO_MFMA", "TR_MNL_SPI")}
+    saved = {k: os.environ.get(k) for k in ("TR_FORCE_TWOPASS", "TR_NO_MFMA", "TR_MNL_SPI", "TR_MNL_DUO")}
     for k in saved:
         os.environ.pop(k, None)
     if kind == "twopass":
@@ -46,6 +47,9 @@ def path(kind):
         os.environ["TR_NO_MFMA"] = "1"
     if kind == "spi1":
         os.environ["TR_MNL_SPI"] = "1"
+        os.environ["TR_MNL_DUO"] = "0"
+    if kind == "noduo":
+        os.environ["TR_MNL_DUO"] = "0"
     S._plan_cache.clear()
     try:
         yield
@@ -142,7 +146,7 @@ def test_linear_golden(name, kind):
             _assert_factors(model.Bcp, d["Bcp_final2_list"])
 
 
-@pytest.mark.parametrize("kind", ["auto", "spi1", "twopass", "valu"])
+@pytest.mark.parametrize("kind", ["auto", "noduo", "spi1", "twopass", "valu"])
 @pytest.mark.parametrize("name", MNL)
 def test_multinomial_golden(name, kind):
     with path(kind):
@@ -336,13 +340,16 @@ MNL_SHAPES = [((50, 8, 4), 2, 2), ((200, 16, 8), 10, 4), ((97, 5, 7), 16, 3), ((
               # fewer samples than workgroups, the config-3 sample shape, one class
               ((300, 100, 12), 7, 5), ((257, 64, 128), 4, 8), ((100, 128, 64), 10, 8), ((700, 72, 40), 3, 3),
               ((90, 8, 8), 1, 2),
+              # two-workgroups-per-CU variant: R % 4 != 0 over two rank blocks, one rank block,
+              # fewer samples than workgroups, J = 128
+              ((1001, 128, 64), 10, 5), ((513, 128, 64), 16, 3), ((2, 128, 64), 2, 8), ((300, 64, 128), 6, 7),
               # wide classes (C > 16): logits by class tile (MFMA when P % 32 == 0, else VALU),
               # k_softmax_rows, tiled column reduction; rank beyond 64 (MTTKRP rank tiles)
               ((150, 8, 4), 17, 3), ((230, 16, 8), 40, 5), ((99, 5, 7), 33, 2), ((200, 12), 100, 4),
               ((120, 6, 5), 5, 70), ((80, 4, 8), 20, 130)]
 
 
-@pytest.mark.parametrize("kind", ["auto", "spi1", "twopass", "valu"])
+@pytest.mark.parametrize("kind", ["auto", "noduo", "spi1", "twopass", "valu"])
 @pytest.mark.parametrize("shape,C,rank", MNL_SHAPES)
 def test_multinomial_sweep_vs_oracle(shape, C, rank, kind):
     with path(kind):
