@@ -20,6 +20,7 @@
 // slots, the summation orders and the slab accumulation order are those of k_mnl_fused.
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 #include "tr_common.h"
 #include "tr_mnl.h"
@@ -104,17 +105,31 @@ struct DuArgs {
   int reverse;
 };
 
-// ROLE 0: A-wave (i block, j block) -> T for both rank blocks; ROLE 1: B-wave -> V
-template <int ROLE, int NRB>
+// One LDS-DMA piece per lane with a scalar base: 16 B from sbase + voff (bytes, per lane) to LDS
+// byte address m0v + 16 * lane.  No per-piece 64-bit address arithmetic; m0 is compiler-reserved
+// and is saved / restored inside the statement.
+__device__ __forceinline__ void du_dma_s(uint32_t voff, const float* sbase, uint32_t m0v) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(sbase), "s"(m0v)
+               : "memory");
+}
+
+// ROLE 0: A-wave (i block, j block) -> T for both rank blocks; ROLE 1: B-wave -> V.
+// Shape fixed at compile time: J = JT (64 or 128), I = 8192 / JT (a 32 KiB sample, two 64-row
+// blocks), every LDS-DMA group valid, chunk swizzle q ^ (i & 15).
+template <int ROLE, int NRB, int JT>
 __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, const int64_t* __restrict__ lab,
                                          const float* __restrict__ class_w, float* lds, const int wv, const int lane) {
   const int t = threadIdx.x;
-  const int I = g.I, J = g.J, R = g.R, C = g.C;
+  constexpr int J = JT, I = 8192 / JT, SPF = 8192, JQ = J / 4;
+  constexpr int NJB = J / 64, NIB = I / 64;
+  const int R = g.R, C = g.C;
   constexpr int nrb = NRB;  // rank blocks of 4 (1 or 2)
-  const int SPF = I * J;
   float* sZ = lds + g.du_oZ;    // [2 parity][16 classes][4 A-unit slots]
-  float* sP1 = lds + g.du_oP1;  // Phi1^T [R][J + 4] (A-waves' B operand, 4 consecutive k per b128)
-  const int P1S = J + 4;
+  float* sP1 = lds + g.du_oP1;  // Phi1^T [4 nrb][J + 4] (A-waves' B operand, 4 consecutive k per b128)
+  constexpr int P1S = J + 4;
   const float* P0 = a.phi;
   const float* P1 = a.phi + g.offP1;
   const float* PC = a.phi + g.offPC;
@@ -122,15 +137,18 @@ __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, cons
   const bool cok = c < C;
   const float cwl = cok ? class_w[c] : 0.f;  // class weight of class c in lane c of every row
   const float NEG = -__builtin_huge_valf();
-  float sel[4];  // 1 where l & 3 == q
+  float sel[4], gsel[4];  // 1 where l & 3 == q / where the DPP row (l >> 4) == q
 #pragma unroll
-  for (int q = 0; q < 4; ++q) sel[q] = l3 == q ? 1.f : 0.f;
+  for (int q = 0; q < 4; ++q) {
+    sel[q] = l3 == q ? 1.f : 0.f;
+    gsel[q] = grow == q ? 1.f : 0.f;
+  }
 
   // (i, j) block of this wave: A-units of k_mnl_fused number rb + nrb * (jb + njb * ib), B-units
   // rb + nrb * (ib + nib * jb); a wave here is one (ib, jb) set with every rank block
   const int s = ROLE == 0 ? wv : wv - 2;
-  const int ib = ROLE == 0 ? s / g.njb : s % g.nib;
-  const int jb = ROLE == 0 ? s % g.njb : s / g.nib;
+  const int ib = ROLE == 0 ? s / NJB : s % NIB;
+  const int jb = ROLE == 0 ? s % NJB : s / NIB;
 
   // per rank block rb: rank of this lane's accumulator column, factor registers
   float phiU[2][4], wpc[2][4], pcg[2], wg[2];
@@ -161,25 +179,32 @@ __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, cons
   }
   for (int e = t; e < 2 * 16 * 4; e += DU_T) sZ[e] = 0.f;
 
-  // LDS-DMA map: wave wv issues the 1 KiB groups wv + 4 gi of every sample
-  const int ngroups = g.nchunk / TR_WAVE;  // (full shapes: nchunk % 64 == 0)
-  const int gcnt = ngroups > wv ? (ngroups - wv + DU_NW - 1) / DU_NW : 0;
-  int goff[DU_GMAX];
+  // LDS-DMA map: wave wv issues the 1 KiB groups wv + 4 gi (gi < 8) of every sample; LDS bytes
+  // of group G at ring slot b: 32 KiB b + 1 KiB G
+  uint32_t goff[8];
 #pragma unroll
-  for (int gi = 0; gi < DU_GMAX; ++gi) {
+  for (int gi = 0; gi < 8; ++gi) {
     const int slot = (wv + DU_NW * gi) * TR_WAVE + lane;
-    const int i = slot / g.JQ;
-    const int q = slot - i * g.JQ;
-    goff[gi] = gi < gcnt ? i * J + 4 * (q ^ (i & g.smask)) : 0;
+    const int i = slot / JQ;
+    const int q = slot - i * JQ;
+    goff[gi] = 4u * (uint32_t)(i * J + 4 * (q ^ (i & 15)));
   }
+  const uint32_t lbase = (uint32_t)__builtin_amdgcn_readfirstlane(
+      (int)(uint32_t)(uintptr_t)((const __attribute__((address_space(3))) float*)lds));
+  // LDS read offsets (floats) of this lane's operand quads: A-wave quad c4 of its row at
+  // aoff[c4]; B-wave quad of step st at boff[st & 3] + 4 J st
+  int aoff[16], boff[4];
+#pragma unroll
+  for (int c4 = 0; c4 < 16; ++c4) aoff[c4] = (64 * ib + lane) * J + 64 * jb + 4 * (c4 ^ c);
+#pragma unroll
+  for (int m = 0; m < 4; ++m) boff[m] = (64 * ib + grow) * J + 64 * jb + 4 * (c ^ (4 * m + grow));
+  const int pb0 = l3 * P1S + 64 * jb, pb1 = ((nrb > 1 ? 4 : 0) + l3) * P1S + 64 * jb;
+
   const int64_t n0 = (int64_t)blockIdx.x * a.rows_per_wg;
   const int64_t n1 = n0 + a.rows_per_wg < a.N ? n0 + a.rows_per_wg : a.N;
   const int nr = (int)(n1 > n0 ? n1 - n0 : 0);
   auto sample_of = [&](int k) -> int64_t { return a.reverse ? (n1 - 1 - k) : (n0 + k); };
-  auto issue = [&](const float* src, float* dst, int gi) {
-    if (gi < gcnt) du_dma16(src + goff[gi], dst + DU_NW * gi * 256);
-  };
-  auto dst_of = [&](int buf) { return lds + buf * SPF + wv * 256; };
+  auto src_of = [&](int k) -> const float* { return a.X + sample_of(k) * a.xld; };
 
   __syncthreads();
   __builtin_amdgcn_s_waitcnt(0);  // retire the prologue's loads (the loop waits are counted)
@@ -202,7 +227,7 @@ __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, cons
       uP[rb][q] = 0.f;
     }
   }
-  int64_t yP = 0;
+  int64_t yP = 0;  // label / class weight of the sample in the epilogue
   float cwP = 0.f;
 
   // ---- epilogue of one sample, in 8 stages (the chain of dependent steps is cut so that the
@@ -269,7 +294,7 @@ __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, cons
       for (int rb = 0; rb < NRB; ++rb) {
         if (ROLE == 0) {
           gacc[rb][0] += e_wv[rb] * accP[rb][0];
-          const float ug = grow == 0 ? uP[rb][0] : grow == 1 ? uP[rb][1] : grow == 2 ? uP[rb][2] : uP[rb][3];
+          const float ug = fmaf(uP[rb][3], gsel[3], fmaf(uP[rb][2], gsel[2], fmaf(uP[rb][1], gsel[1], uP[rb][0] * gsel[0])));
           dpc[rb] = fmaf(e_dz, wg[rb] * ug, dpc[rb]);
         } else {
 #pragma unroll
@@ -280,59 +305,71 @@ __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, cons
   };
 
   if (nr > 0) {
-    const float* src = a.X + sample_of(0) * a.xld;
+    const float* src = src_of(0);
 #pragma unroll
-    for (int gi = 0; gi < DU_GMAX; ++gi) issue(src, dst_of(0), gi);
+    for (int gi = 0; gi < 8; ++gi) du_dma_s(goff[gi], src, lbase + (uint32_t)(wv + DU_NW * gi) * 1024u);
   }
-  // iteration k: barrier -> GEMM of sample k with the epilogue of k - 1 between its steps and
-  // the LDS-DMA of k + 1 into the other ring slot; the epilogue of the last sample after the loop
-  for (int k = 0; k < nr; ++k) {
+  int64_t yN = nr > 0 ? lab[sample_of(0)] : 0;  // label of the next GEMM sample (scalar, one ahead)
+
+  // iteration k (ring slot SL = k & 1, a compile-time constant: the loop is unrolled by two so
+  // every LDS read is a base register + immediate): barrier -> GEMM of sample k with the
+  // epilogue of k - 1 between its steps and the LDS-DMA of k + 1 into the other slot (of sample k
+  // itself when k is the last one: a harmless refill of a free slot, no guard per piece)
+  auto iter = [&](auto slot_c, int k) {
+    constexpr int SL = decltype(slot_c)::value;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // own pieces of sample k
-    du_barrier();  // everyone's pieces of k; Z partials of k - 1; slot (k + 1) & 1 free
-    const bool pre = k + 1 < nr && !(TR_DUO_SKIP & 1);
-    const float* psrc = pre ? a.X + sample_of(k + 1) * a.xld : a.X;
-    float* pdst = dst_of((k + 1) & 1);
-    const int zs = (k - 1) & 1;
-    const int64_t yC = lab[sample_of(k)];
+    du_barrier();  // everyone's pieces of k; Z partials of k - 1; slot SL ^ 1 free
+    const int64_t yC = yN;
     const float cwC = du_rdl(cwl, (int)yC);
-    epi(0, zs, yP, cwP);
-    const float* sb = lds + (k & 1) * SPF;
+    const bool more = k + 1 < nr;
+    yN = lab[sample_of(more ? k + 1 : k)];
+    const float* psrc = (more && !(TR_DUO_SKIP & 1)) ? src_of(k + 1) : src_of(k);
+    const uint32_t pm0 = lbase + (uint32_t)((SL ^ 1) * 4 * SPF) + (uint32_t)wv * 1024u;
+    epi(0, SL ^ 1, yP, cwP);
+    const float* sb = lds + SL * SPF;
     du_f32x4 acc[2][4];
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
       for (int q = 0; q < 4; ++q) acc[rb][q] = du_f32x4{0.f, 0.f, 0.f, 0.f};
-    if (ROLE == 0) {
-      const int row = 64 * ib + lane;
-      const float* rp = sb + row * J;
-      const int sw = row & g.smask;
-      const float* bp0 = sP1 + (0 + l3) * P1S + 64 * jb;
-      const float* bp1 = sP1 + ((nrb > 1 ? 4 : 0) + l3) * P1S + 64 * jb;
-      float4 xr[16];  // operand quads read XL steps ahead (bounded live registers)
-      auto ldA = [&](int c4) { xr[c4] = *reinterpret_cast<const float4*>(rp + 4 * ((16 * jb + c4) ^ sw)); };
+    float4 xr[16];  // operand quads read XL steps ahead (bounded live registers)
+    auto ld = [&](int st) {
+      if (ROLE == 0)
+        xr[st] = *reinterpret_cast<const float4*>(sb + aoff[st]);
+      else
+        xr[st] = *reinterpret_cast<const float4*>(sb + boff[st & 3] + 4 * J * st);
+    };
 #pragma unroll
-      for (int c4 = 0; c4 < XL; ++c4) ldA(c4);
+    for (int st = 0; st < XL; ++st) ld(st);
 #pragma unroll
-      for (int c4 = 0; c4 < 16; ++c4) {
-        if (c4 + XL < 16) ldA(c4 + XL);
-        if ((c4 & 1) == 0 && pre) issue(psrc, pdst, c4 >> 1);
-        const float4 b0 = *reinterpret_cast<const float4*>(bp0 + 4 * c4);
-        acc[0][0] = du_mfma(xr[c4].x, b0.x, acc[0][0]);
-        acc[0][1] = du_mfma(xr[c4].y, b0.y, acc[0][1]);
-        acc[0][2] = du_mfma(xr[c4].z, b0.z, acc[0][2]);
-        acc[0][3] = du_mfma(xr[c4].w, b0.w, acc[0][3]);
+    for (int st = 0; st < 16; ++st) {
+      if (st + XL < 16) ld(st + XL);
+      if ((st & 1) == 0) du_dma_s(goff[st >> 1], psrc, pm0 + (uint32_t)(st >> 1) * 4096u);
+      if (ROLE == 0) {
+        const float4 b0 = *reinterpret_cast<const float4*>(sP1 + pb0 + 4 * st);
+        acc[0][0] = du_mfma(xr[st].x, b0.x, acc[0][0]);
+        acc[0][1] = du_mfma(xr[st].y, b0.y, acc[0][1]);
+        acc[0][2] = du_mfma(xr[st].z, b0.z, acc[0][2]);
+        acc[0][3] = du_mfma(xr[st].w, b0.w, acc[0][3]);
         if (nrb > 1) {
-          const float4 b1 = *reinterpret_cast<const float4*>(bp1 + 4 * c4);
-          acc[1][0] = du_mfma(xr[c4].x, b1.x, acc[1][0]);
-          acc[1][1] = du_mfma(xr[c4].y, b1.y, acc[1][1]);
-          acc[1][2] = du_mfma(xr[c4].z, b1.z, acc[1][2]);
-          acc[1][3] = du_mfma(xr[c4].w, b1.w, acc[1][3]);
+          const float4 b1 = *reinterpret_cast<const float4*>(sP1 + pb1 + 4 * st);
+          acc[1][0] = du_mfma(xr[st].x, b1.x, acc[1][0]);
+          acc[1][1] = du_mfma(xr[st].y, b1.y, acc[1][1]);
+          acc[1][2] = du_mfma(xr[st].z, b1.z, acc[1][2]);
+          acc[1][3] = du_mfma(xr[st].w, b1.w, acc[1][3]);
         }
-        if ((c4 & 1) == 1 && c4 < 15) epi(1 + (c4 >> 1), zs, yP, cwP);
-      }
-      if (pre)
+      } else {
 #pragma unroll
-        for (int gi = 8; gi < DU_GMAX; ++gi) issue(psrc, pdst, gi);
+        for (int rb = 0; rb < nrb; ++rb) {
+          acc[rb][0] = du_mfma(xr[st].x, bopB[rb][st], acc[rb][0]);
+          acc[rb][1] = du_mfma(xr[st].y, bopB[rb][st], acc[rb][1]);
+          acc[rb][2] = du_mfma(xr[st].z, bopB[rb][st], acc[rb][2]);
+          acc[rb][3] = du_mfma(xr[st].w, bopB[rb][st], acc[rb][3]);
+        }
+      }
+      if ((st & 1) == 1 && st < 15) epi(1 + (st >> 1), SL ^ 1, yP, cwP);
+    }
+    if (ROLE == 0) {
 #pragma unroll
       for (int rb = 0; rb < nrb; ++rb) {
         const du_f32x4 T = (acc[rb][0] + acc[rb][1]) + (acc[rb][2] + acc[rb][3]);
@@ -353,33 +390,10 @@ __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, cons
         zpart = fmaf(wpc[rb][1], uP[rb][1], zpart);
         zpart = fmaf(wpc[rb][2], uP[rb][2], zpart);
         zpart = fmaf(wpc[rb][3], uP[rb][3], zpart);
-        if (lane < 16) sZ[((k & 1) * 16 + lane) * 4 + rb + nrb * s] = zpart;
+        // every row holds the same 16 class partials: all four rows store (same value, same slot)
+        sZ[(SL * 16 + c) * 4 + rb + nrb * s] = zpart;
       }
     } else {
-      const int cq = 16 * jb + c;
-      float4 xr[16];  // operand quads read XL steps ahead (bounded live registers)
-      auto ldB = [&](int st) {
-        const int i = 64 * ib + 4 * st + grow;
-        xr[st] = *reinterpret_cast<const float4*>(sb + i * J + 4 * (cq ^ (i & g.smask)));
-      };
-#pragma unroll
-      for (int st = 0; st < XL; ++st) ldB(st);
-#pragma unroll
-      for (int st = 0; st < 16; ++st) {
-        if (st + XL < 16) ldB(st + XL);
-        if ((st & 1) == 0 && pre) issue(psrc, pdst, st >> 1);
-#pragma unroll
-        for (int rb = 0; rb < nrb; ++rb) {
-          acc[rb][0] = du_mfma(xr[st].x, bopB[rb][st], acc[rb][0]);
-          acc[rb][1] = du_mfma(xr[st].y, bopB[rb][st], acc[rb][1]);
-          acc[rb][2] = du_mfma(xr[st].z, bopB[rb][st], acc[rb][2]);
-          acc[rb][3] = du_mfma(xr[st].w, bopB[rb][st], acc[rb][3]);
-        }
-        if ((st & 1) == 1 && st < 15) epi(1 + (st >> 1), zs, yP, cwP);
-      }
-      if (pre)
-#pragma unroll
-        for (int gi = 8; gi < DU_GMAX; ++gi) issue(psrc, pdst, gi);
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
@@ -387,7 +401,12 @@ __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, cons
     }
     yP = yC;
     cwP = cwC;
+  };
+  for (int k = 0; k < nr; k += 2) {
+    iter(std::integral_constant<int, 0>(), k);
+    if (k + 1 < nr) iter(std::integral_constant<int, 1>(), k + 1);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last (harmless) refill has landed
   du_barrier();  // Z partials of the last sample
   if (nr > 0) {
 #pragma unroll
@@ -452,7 +471,7 @@ __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, cons
   for (int64_t e = t; e < g.slab; e += DU_T) slab[e] = sG[e];
 }
 
-template <int NRB>
+template <int NRB, int JT>
 __global__ __launch_bounds__(DU_T, 2) void k_mnl_duo(MnlGeom g, DuArgs a, const int64_t* __restrict__ lab,
                                                   const float* __restrict__ class_w, const int32_t* __restrict__ stop) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -460,20 +479,28 @@ __global__ __launch_bounds__(DU_T, 2) void k_mnl_duo(MnlGeom g, DuArgs a, const 
   const int lane = threadIdx.x & (TR_WAVE - 1);
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / TR_WAVE);
   if (wv < 2)
-    duo_body<0, NRB>(g, a, lab, class_w, lds, wv, lane);
+    duo_body<0, NRB, JT>(g, a, lab, class_w, lds, wv, lane);
   else
-    duo_body<1, NRB>(g, a, lab, class_w, lds, wv, lane);
+    duo_body<1, NRB, JT>(g, a, lab, class_w, lds, wv, lane);
 }
 
 // ------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------
+static const void* duo_kernel(const MnlGeom& g) {
+  if (g.J == 64)
+    return g.nrb == 2 ? reinterpret_cast<const void*>(&k_mnl_duo<2, 64>) : reinterpret_cast<const void*>(&k_mnl_duo<1, 64>);
+  return g.nrb == 2 ? reinterpret_cast<const void*>(&k_mnl_duo<2, 128>) : reinterpret_cast<const void*>(&k_mnl_duo<1, 128>);
+}
+
 void mnl_duo_geom(MnlGeom* g) {
   g->duo = 0;
   const char* env = std::getenv("TR_MNL_DUO");
   if (env != nullptr && env[0] == '0') return;
-  if (!g->full || g->nib * g->njb != 2 || g->nrb > 2 || g->C > kMnlCMax) return;
-  if (g->nchunk % TR_WAVE != 0 || g->nchunk / TR_WAVE > DU_NW * DU_GMAX) return;
+  // compiled shapes: a 32 KiB sample as (128, 64) or (64, 128) (two 64-row blocks, 8 LDS-DMA
+  // groups per wave, chunk swizzle q ^ (i & 15))
+  if (!g->full || g->I * g->J != 8192 || (g->J != 64 && g->J != 128) || g->nrb > 2 || g->C > kMnlCMax) return;
+  if (g->smask != 15) return;
   const int64_t spf = (int64_t)g->I * g->J;
   int64_t o = 2 * spf;  // ring of two samples
   g->du_oZ = (int)o;
@@ -491,7 +518,7 @@ void mnl_duo_geom(MnlGeom* g) {
 
 hipError_t mnl_duo_prepare(MnlGeom* g) {
   if (!g->duo) return hipSuccess;
-  const void* k = g->nrb == 2 ? reinterpret_cast<const void*>(&k_mnl_duo<2>) : reinterpret_cast<const void*>(&k_mnl_duo<1>);
+  const void* k = duo_kernel(*g);
   const size_t lds = (size_t)g->du_lds_floats * 4;
   hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
@@ -511,10 +538,19 @@ hipError_t launch_mnl_duo(const MnlGeom& g, int grid, const float* X, int64_t N,
   if (grid < 1 || rows_per_wg < 0 || xld % 4 != 0 || (int64_t)grid * rows_per_wg < N) return hipErrorInvalidValue;
   DuArgs a{X, N, xld, phi, w, scale, gpart, dpart, rows_per_wg, reverse};
   const size_t lds = (size_t)g.du_lds_floats * 4;
-  if (g.nrb == 2)
-    hipLaunchKernelGGL(k_mnl_duo<2>, dim3(grid), dim3(DU_T), lds, st, g, a, lab, class_w, stop);
-  else
-    hipLaunchKernelGGL(k_mnl_duo<1>, dim3(grid), dim3(DU_T), lds, st, g, a, lab, class_w, stop);
+#define TR_DUO_LAUNCH(NRB, JT) hipLaunchKernelGGL((k_mnl_duo<NRB, JT>), dim3(grid), dim3(DU_T), lds, st, g, a, lab, class_w, stop)
+  if (g.J == 64) {
+    if (g.nrb == 2)
+      TR_DUO_LAUNCH(2, 64);
+    else
+      TR_DUO_LAUNCH(1, 64);
+  } else {
+    if (g.nrb == 2)
+      TR_DUO_LAUNCH(2, 128);
+    else
+      TR_DUO_LAUNCH(1, 128);
+  }
+#undef TR_DUO_LAUNCH
   return hipGetLastError();
 }
 
