@@ -25,6 +25,22 @@
 #include "tr_common.h"
 #include "tr_mnl.h"
 
+#ifndef TR_DUO_PROFILE
+#define TR_DUO_PROFILE 0  // profiling build only: per-phase cycle counts of every wave (tools/duo_profile.py)
+#endif
+#if TR_DUO_PROFILE
+__device__ unsigned long long g_duo_prof[512][4][4];
+#define TR_DUO_MARK(ph)                                           \
+  do {                                                            \
+    const unsigned long long _now = __builtin_readcyclecounter(); \
+    prof[ph] += _now - prof_t;                                    \
+    prof_t = _now;                                                \
+  } while (0)
+#else
+#define TR_DUO_MARK(ph) \
+  do {                  \
+  } while (0)
+#endif
 #ifndef TR_DUO_SKIP
 #define TR_DUO_SKIP 0  // profiling ablation only (results invalid): 1 loop LDS-DMA, 2 MFMAs, 4 epilogue
 #endif
@@ -37,7 +53,22 @@ constexpr int DU_T = DU_NW * TR_WAVE;
 #ifndef TR_DUO_XL
 #define TR_DUO_XL 8
 #endif
-constexpr int XL = TR_DUO_XL;  // GEMM steps an operand quad is read ahead of its MFMAs
+constexpr int XL = TR_DUO_XL;  // GEMM steps an operand quad is read ahead of its MFMAs (B-waves)
+#ifndef TR_DUO_DMA_EVERY
+#define TR_DUO_DMA_EVERY 1
+#endif
+constexpr int DMA_EVERY = TR_DUO_DMA_EVERY;  // GEMM steps between the 8 LDS-DMA pieces of the next sample
+#ifndef TR_DUO_EARLY
+#define TR_DUO_EARLY 0
+#endif
+// 1: the LDS-DMA of sample k + 2 is issued as soon as every wave is past the GEMM of k (two
+// barriers per sample, up to two samples in flight per workgroup); 0: the DMA of k + 1 is
+// interleaved with the GEMM of k after the single barrier of iteration k
+constexpr bool EARLY = TR_DUO_EARLY != 0;
+#ifndef TR_DUO_XLA
+#define TR_DUO_XLA 4
+#endif
+constexpr int XLA = TR_DUO_XLA;  // the same for the A-waves (X and Phi1 quads)
 constexpr int DU_GMAX = 12;  // LDS-DMA pieces (1 KiB) per wave per sample (sample <= 48 KiB)
 typedef float du_f32x4 __attribute__((ext_vector_type(4)));
 
@@ -116,19 +147,20 @@ __device__ __forceinline__ void du_dma_s(uint32_t voff, const float* sbase, uint
                : "memory");
 }
 
-// ROLE 0: A-wave (i block, j block) -> T for both rank blocks; ROLE 1: B-wave -> V.
+// Wave wv = (block s = wv & 1, rank block rb = wv >> 1): the T unit AND the V unit of its X
+// sub-block (64 x 64) and rank block, so all four waves carry the same instruction mix (an
+// A/B role split left the T waves on the critical path and the V waves idle at the barrier).
 // Shape fixed at compile time: J = JT (64 or 128), I = 8192 / JT (a 32 KiB sample, two 64-row
-// blocks), every LDS-DMA group valid, chunk swizzle q ^ (i & 15).
-template <int ROLE, int NRB, int JT>
+// blocks), R in 5..8 (two rank blocks), every LDS-DMA group valid, chunk swizzle q ^ (i & 15).
+template <int JT>
 __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, const int64_t* __restrict__ lab,
                                          const float* __restrict__ class_w, float* lds, const int wv, const int lane) {
   const int t = threadIdx.x;
   constexpr int J = JT, I = 8192 / JT, SPF = 8192, JQ = J / 4;
   constexpr int NJB = J / 64, NIB = I / 64;
   const int R = g.R, C = g.C;
-  constexpr int nrb = NRB;  // rank blocks of 4 (1 or 2)
-  float* sZ = lds + g.du_oZ;    // [2 parity][16 classes][4 A-unit slots]
-  float* sP1 = lds + g.du_oP1;  // Phi1^T [4 nrb][J + 4] (A-waves' B operand, 4 consecutive k per b128)
+  float* sZ = lds + g.du_oZ;    // [2 parity][16 classes][4 T-unit slots]
+  float* sP1 = lds + g.du_oP1;  // Phi1^T [8][J + 4] (T units' B operand, 4 consecutive k per b128)
   constexpr int P1S = J + 4;
   const float* P0 = a.phi;
   const float* P1 = a.phi + g.offP1;
@@ -144,36 +176,28 @@ __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, cons
     gsel[q] = grow == q ? 1.f : 0.f;
   }
 
-  // (i, j) block of this wave: A-units of k_mnl_fused number rb + nrb * (jb + njb * ib), B-units
-  // rb + nrb * (ib + nib * jb); a wave here is one (ib, jb) set with every rank block
-  const int s = ROLE == 0 ? wv : wv - 2;
-  const int ib = ROLE == 0 ? s / NJB : s % NIB;
-  const int jb = ROLE == 0 ? s % NJB : s / NIB;
-
-  // per rank block rb: rank of this lane's accumulator column, factor registers
-  float phiU[2][4], wpc[2][4], pcg[2], wg[2];
-  float bopB[2][16];  // B-waves: Phi0[64 ib + 4 st + grow][rq]
+  const int s = wv & 1, rb = wv >> 1;
+  const int ib = NIB == 2 ? s : 0, jb = NJB == 2 ? s : 0;
+  const int rq = 4 * rb + l3;  // rank of this lane's accumulator column
+  const bool rqv = rq < R;
+  // T unit: U partial weights phiU[v] = Phi0[64 ib + 4 (l >> 2) + v][rq], Z partial weights
+  // wpc[v] = w_r PhiC[c][r] (r = 4 rb + v); epilogue weights pcg = w_r PhiC[c][r] (r = 4 rb + row)
+  // V unit: B operand bopB[st] = Phi0[64 ib + 4 st + row][rq]
+  float phiU[4], wpc[4], bopB[16];
 #pragma unroll
-  for (int rb = 0; rb < 2; ++rb) {
-    const int rq = 4 * rb + l3;
-    const bool ok = rb < nrb && rq < R;
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const int row = 64 * ib + 4 * (lane >> 2) + v;
-      phiU[rb][v] = (ROLE == 0 && ok) ? P0[(int64_t)row * R + rq] : 0.f;
-      const int r = 4 * rb + v;
-      wpc[rb][v] = (ROLE == 0 && rb < nrb && cok && r < R) ? a.w[r] * PC[c * R + r] : 0.f;
-    }
-    const int r = 4 * rb + grow;
-    pcg[rb] = (rb < nrb && cok && r < R) ? a.w[r] * PC[c * R + r] : 0.f;
-    wg[rb] = (rb < nrb && r < R) ? a.w[r] : 0.f;
-#pragma unroll
-    for (int st = 0; st < 16; ++st)
-      bopB[rb][st] = (ROLE == 1 && ok) ? P0[(int64_t)(64 * ib + 4 * st + grow) * R + rq] : 0.f;
+  for (int v = 0; v < 4; ++v) {
+    phiU[v] = rqv ? P0[(int64_t)(64 * ib + 4 * (lane >> 2) + v) * R + rq] : 0.f;
+    const int r = 4 * rb + v;
+    wpc[v] = (cok && r < R) ? a.w[r] * PC[c * R + r] : 0.f;
   }
-  // Phi1^T table (A-waves' B operands), rank rows padded to 4 nrb with zeros (a padded rank's
-  // T column must stay finite: U sums every lane's column times phiU, which is 0 there)
-  for (int e = t; e < 4 * nrb * J; e += DU_T) {
+  const int rg = 4 * rb + grow;
+  const float pcg = (cok && rg < R) ? a.w[rg] * PC[c * R + rg] : 0.f;
+  const float wg = rg < R ? a.w[rg] : 0.f;
+#pragma unroll
+  for (int st = 0; st < 16; ++st) bopB[st] = rqv ? P0[(int64_t)(64 * ib + 4 * st + grow) * R + rq] : 0.f;
+  // Phi1^T table, rank rows padded to 8 with zeros (a padded rank's T column must stay finite:
+  // U sums every lane's column times phiU, which is 0 there)
+  for (int e = t; e < 8 * J; e += DU_T) {
     const int r = e / J, j = e - r * J;
     sP1[r * P1S + j] = r < R ? P1[(int64_t)j * R + r] : 0.f;
   }
@@ -191,14 +215,14 @@ __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, cons
   }
   const uint32_t lbase = (uint32_t)__builtin_amdgcn_readfirstlane(
       (int)(uint32_t)(uintptr_t)((const __attribute__((address_space(3))) float*)lds));
-  // LDS read offsets (floats) of this lane's operand quads: A-wave quad c4 of its row at
-  // aoff[c4]; B-wave quad of step st at boff[st & 3] + 4 J st
+  // LDS read offsets (floats): T quad c4 of this lane's row at aoff[c4]; V quad of step st at
+  // boff[st & 3] + 4 J st; Phi1 quad of step st at pb + 4 st
   int aoff[16], boff[4];
 #pragma unroll
   for (int c4 = 0; c4 < 16; ++c4) aoff[c4] = (64 * ib + lane) * J + 64 * jb + 4 * (c4 ^ c);
 #pragma unroll
   for (int m = 0; m < 4; ++m) boff[m] = (64 * ib + grow) * J + 64 * jb + 4 * (c ^ (4 * m + grow));
-  const int pb0 = l3 * P1S + 64 * jb, pb1 = ((nrb > 1 ? 4 : 0) + l3) * P1S + 64 * jb;
+  const int pb = rq * P1S + 64 * jb;
 
   const int64_t n0 = (int64_t)blockIdx.x * a.rows_per_wg;
   const int64_t n1 = n0 + a.rows_per_wg < a.N ? n0 + a.rows_per_wg : a.N;
@@ -209,24 +233,18 @@ __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, cons
   __syncthreads();
   __builtin_amdgcn_s_waitcnt(0);  // retire the prologue's loads (the loop waits are counted)
 
-  du_f32x4 gacc[2][4];  // A: gacc[rb][0] (dPhi0 rows x ranks); B: all four (dPhi1 by row class)
+  du_f32x4 gT = du_f32x4{0.f, 0.f, 0.f, 0.f};  // dPhi0 rows x ranks of the T unit
+  du_f32x4 gV[4];                                // dPhi1 of the V unit, by row class
 #pragma unroll
-  for (int rb = 0; rb < 2; ++rb)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) gacc[rb][q] = du_f32x4{0.f, 0.f, 0.f, 0.f};
-  float dpc[2] = {0.f, 0.f};  // A: dPhiC[c][4 rb + grow]
+  for (int q = 0; q < 4; ++q) gV[q] = du_f32x4{0.f, 0.f, 0.f, 0.f};
+  float dpc = 0.f;  // dPhiC[c][4 rb + row] of the T unit
   double lsum = 0.0;
 
-  du_f32x4 accP[2][4];  // previous sample's GEMM output (A: accP[rb][0] = T; B: V by row class)
-  float uP[2][4];
+  du_f32x4 TP = du_f32x4{0.f, 0.f, 0.f, 0.f};  // previous sample's T (summed) and V (by row class)
+  du_f32x4 VP[4];
 #pragma unroll
-  for (int rb = 0; rb < 2; ++rb) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      accP[rb][q] = du_f32x4{0.f, 0.f, 0.f, 0.f};
-      uP[rb][q] = 0.f;
-    }
-  }
+  for (int q = 0; q < 4; ++q) VP[q] = du_f32x4{0.f, 0.f, 0.f, 0.f};
+  float uP[4] = {0.f, 0.f, 0.f, 0.f};
   int64_t yP = 0;  // label / class weight of the sample in the epilogue
   float cwP = 0.f;
 
@@ -237,12 +255,11 @@ __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, cons
   // Wv[r] = sum_c dZ[c] w_r PhiC[c, r].  Every sum over the 16 classes that the chain needs after
   // S is formed at once (independent DPP row sums, so their latencies overlap):
   //   s2 = sum q, d1 = sum S q, e1 = S_y, a_r = sum S q p_r, b_r = sum S p_r, y_r = S_y p_{y,r}
-  // with q = exp(S), p_r = w_r PhiC[., r]; then <dS, S> = k (d1 / s2 - e1) and
-  // Wv[r] = k (a_r / s2 - y_r) - <dS, S> b_r  (k = cw_y / W).
+  // with q = exp(S), p_r = w_r PhiC[., r] (r = 4 rb + row: this wave's rank block); then
+  // <dS, S> = k (d1 / s2 - e1) and Wv[r] = k (a_r / s2 - y_r) - <dS, S> b_r  (k = cw_y / W).
   float4 e_zp = make_float4(0.f, 0.f, 0.f, 0.f);
   float e_x = 0.f, e_ez = 0.f, e_sum = 0.f, e_S = 0.f, e_q = 0.f, e_Sq = 0.f, e_Sy = 0.f;
-  float e_s2 = 0.f, e_d1 = 0.f, e_e1 = 0.f, e_dz = 0.f;
-  float e_ar[NRB], e_br[NRB], e_yr[NRB], e_wr[NRB], e_wv[NRB];
+  float e_s2 = 0.f, e_d1 = 0.f, e_e1 = 0.f, e_dz = 0.f, e_ar = 0.f, e_br = 0.f, e_yr = 0.f, e_wr = 0.f, e_wv = 0.f;
   bool e_isy = false;
   // epilogue stage st of the sample with Z partials in parity slot zs, label yE, class weight cwE
   // (for the first call of a workgroup: zero partials, zero accumulators, cwE = 0 -> adds 0)
@@ -266,48 +283,42 @@ __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, cons
       e_s2 = du_row_sum16(e_q);
       e_d1 = du_row_sum16(e_Sq);
       e_e1 = du_row_sum16(e_Sy);
-#pragma unroll
-      for (int rb = 0; rb < NRB; ++rb) {
-        e_ar[rb] = du_row_sum16(e_Sq * pcg[rb]);
-        e_br[rb] = du_row_sum16(e_S * pcg[rb]);
-        e_yr[rb] = du_row_sum16(e_Sy * pcg[rb]);
-      }
+      e_ar = du_row_sum16(e_Sq * pcg);
+      e_br = du_row_sum16(e_S * pcg);
+      e_yr = du_row_sum16(e_Sy * pcg);
     } else if (st == 5) {
       const float is2 = __builtin_amdgcn_rcpf(e_s2);
       const float kk = cwE * a.scale;
       const float dot = kk * (e_d1 * is2 - e_e1);
-      if (ROLE == 0) lsum += (wv == 0 && lane == 0) ? (double)cwE * (double)(du_log(e_s2) - e_e1) : 0.0;
+      lsum += (wv == 0 && lane == 0) ? (double)cwE * (double)(du_log(e_s2) - e_e1) : 0.0;
       const float dS = cok ? kk * (e_q * is2 - (e_isy ? 1.0f : 0.0f)) : 0.f;
       e_dz = cok ? e_S * (dS - dot) : 0.f;
-#pragma unroll
-      for (int rb = 0; rb < NRB; ++rb) e_wr[rb] = kk * (e_ar[rb] * is2 - e_yr[rb]) - dot * e_br[rb];
+      e_wr = kk * (e_ar * is2 - e_yr) - dot * e_br;
     } else if (st == 6) {
       // Wv[4 rb + g] in DPP row g -> lane rank 4 rb + (l & 3) by 0/1 lane masks (no branches)
-#pragma unroll
-      for (int rb = 0; rb < NRB; ++rb) {
-        const float w0 = du_rdl(e_wr[rb], 0), w1 = du_rdl(e_wr[rb], 16), w2 = du_rdl(e_wr[rb], 32),
-                    w3 = du_rdl(e_wr[rb], 48);
-        e_wv[rb] = fmaf(w3, sel[3], fmaf(w2, sel[2], fmaf(w1, sel[1], w0 * sel[0])));
-      }
+      const float w0 = du_rdl(e_wr, 0), w1 = du_rdl(e_wr, 16), w2 = du_rdl(e_wr, 32), w3 = du_rdl(e_wr, 48);
+      e_wv = fmaf(w3, sel[3], fmaf(w2, sel[2], fmaf(w1, sel[1], w0 * sel[0])));
     } else {
+      gT += e_wv * TP;
+      const float ug = fmaf(uP[3], gsel[3], fmaf(uP[2], gsel[2], fmaf(uP[1], gsel[1], uP[0] * gsel[0])));
+      dpc = fmaf(e_dz, wg * ug, dpc);
 #pragma unroll
-      for (int rb = 0; rb < NRB; ++rb) {
-        if (ROLE == 0) {
-          gacc[rb][0] += e_wv[rb] * accP[rb][0];
-          const float ug = fmaf(uP[rb][3], gsel[3], fmaf(uP[rb][2], gsel[2], fmaf(uP[rb][1], gsel[1], uP[rb][0] * gsel[0])));
-          dpc[rb] = fmaf(e_dz, wg[rb] * ug, dpc[rb]);
-        } else {
-#pragma unroll
-          for (int qq = 0; qq < 4; ++qq) gacc[rb][qq] += e_wv[rb] * accP[rb][qq];
-        }
-      }
+      for (int qq = 0; qq < 4; ++qq) gV[qq] += e_wv * VP[qq];
     }
   };
 
-  if (nr > 0) {
-    const float* src = src_of(0);
+#if TR_DUO_PROFILE
+  unsigned long long prof[4] = {0, 0, 0, 0};
+  unsigned long long prof_t = __builtin_readcyclecounter();
+#endif
+  auto dma_sample = [&](const float* src, int slot) {
 #pragma unroll
-    for (int gi = 0; gi < 8; ++gi) du_dma_s(goff[gi], src, lbase + (uint32_t)(wv + DU_NW * gi) * 1024u);
+    for (int gi = 0; gi < 8; ++gi)
+      du_dma_s(goff[gi], src, lbase + (uint32_t)(slot * 4 * SPF) + (uint32_t)(wv + DU_NW * gi) * 1024u);
+  };
+  if (nr > 0) {
+    dma_sample(src_of(0), 0);
+    if (EARLY) dma_sample(src_of(nr > 1 ? 1 : 0), 1);
   }
   int64_t yN = nr > 0 ? lab[sample_of(0)] : 0;  // label of the next GEMM sample (scalar, one ahead)
 
@@ -317,8 +328,13 @@ __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, cons
   // itself when k is the last one: a harmless refill of a free slot, no guard per piece)
   auto iter = [&](auto slot_c, int k) {
     constexpr int SL = decltype(slot_c)::value;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // own pieces of sample k
+    if (EARLY)  // own pieces of sample k (those of k + 1, issued after them, may be in flight)
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    TR_DUO_MARK(0);
     du_barrier();  // everyone's pieces of k; Z partials of k - 1; slot SL ^ 1 free
+    TR_DUO_MARK(1);
     const int64_t yC = yN;
     const float cwC = du_rdl(cwl, (int)yC);
     const bool more = k + 1 < nr;
@@ -327,85 +343,79 @@ __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, cons
     const uint32_t pm0 = lbase + (uint32_t)((SL ^ 1) * 4 * SPF) + (uint32_t)wv * 1024u;
     epi(0, SL ^ 1, yP, cwP);
     const float* sb = lds + SL * SPF;
-    du_f32x4 acc[2][4];
+    du_f32x4 aT[4], aV[4];
 #pragma unroll
-    for (int rb = 0; rb < 2; ++rb)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) acc[rb][q] = du_f32x4{0.f, 0.f, 0.f, 0.f};
-    float4 xr[16];  // operand quads read XL steps ahead (bounded live registers)
-    auto ld = [&](int st) {
-      if (ROLE == 0)
-        xr[st] = *reinterpret_cast<const float4*>(sb + aoff[st]);
-      else
-        xr[st] = *reinterpret_cast<const float4*>(sb + boff[st & 3] + 4 * J * st);
+    for (int q = 0; q < 4; ++q) aT[q] = aV[q] = du_f32x4{0.f, 0.f, 0.f, 0.f};
+    // operand quads read ahead of their MFMAs (bounded live registers)
+    float4 xt[16], bq[16], xv[16];
+    auto ldT = [&](int st) {
+      xt[st] = *reinterpret_cast<const float4*>(sb + aoff[st]);
+      bq[st] = *reinterpret_cast<const float4*>(sP1 + pb + 4 * st);
     };
+    auto ldV = [&](int st) { xv[st] = *reinterpret_cast<const float4*>(sb + boff[st & 3] + 4 * J * st); };
 #pragma unroll
-    for (int st = 0; st < XL; ++st) ld(st);
+    for (int st = 0; st < XLA; ++st) ldT(st);
+#pragma unroll
+    for (int st = 0; st < XL; ++st) ldV(st);
 #pragma unroll
     for (int st = 0; st < 16; ++st) {
-      if (st + XL < 16) ld(st + XL);
-      if ((st & 1) == 0) du_dma_s(goff[st >> 1], psrc, pm0 + (uint32_t)(st >> 1) * 4096u);
-      if (ROLE == 0) {
-        const float4 b0 = *reinterpret_cast<const float4*>(sP1 + pb0 + 4 * st);
-        acc[0][0] = du_mfma(xr[st].x, b0.x, acc[0][0]);
-        acc[0][1] = du_mfma(xr[st].y, b0.y, acc[0][1]);
-        acc[0][2] = du_mfma(xr[st].z, b0.z, acc[0][2]);
-        acc[0][3] = du_mfma(xr[st].w, b0.w, acc[0][3]);
-        if (nrb > 1) {
-          const float4 b1 = *reinterpret_cast<const float4*>(sP1 + pb1 + 4 * st);
-          acc[1][0] = du_mfma(xr[st].x, b1.x, acc[1][0]);
-          acc[1][1] = du_mfma(xr[st].y, b1.y, acc[1][1]);
-          acc[1][2] = du_mfma(xr[st].z, b1.z, acc[1][2]);
-          acc[1][3] = du_mfma(xr[st].w, b1.w, acc[1][3]);
-        }
-      } else {
-#pragma unroll
-        for (int rb = 0; rb < nrb; ++rb) {
-          acc[rb][0] = du_mfma(xr[st].x, bopB[rb][st], acc[rb][0]);
-          acc[rb][1] = du_mfma(xr[st].y, bopB[rb][st], acc[rb][1]);
-          acc[rb][2] = du_mfma(xr[st].z, bopB[rb][st], acc[rb][2]);
-          acc[rb][3] = du_mfma(xr[st].w, bopB[rb][st], acc[rb][3]);
-        }
-      }
+      if (st + XLA < 16) ldT(st + XLA);
+      if (st + XL < 16) ldV(st + XL);
+      if (!EARLY && st % DMA_EVERY == 0 && st / DMA_EVERY < 8)
+        du_dma_s(goff[st / DMA_EVERY], psrc, pm0 + (uint32_t)(st / DMA_EVERY) * 4096u);
+      aT[0] = du_mfma(xt[st].x, bq[st].x, aT[0]);
+      aT[1] = du_mfma(xt[st].y, bq[st].y, aT[1]);
+      aT[2] = du_mfma(xt[st].z, bq[st].z, aT[2]);
+      aT[3] = du_mfma(xt[st].w, bq[st].w, aT[3]);
+      aV[0] = du_mfma(xv[st].x, bopB[st], aV[0]);
+      aV[1] = du_mfma(xv[st].y, bopB[st], aV[1]);
+      aV[2] = du_mfma(xv[st].z, bopB[st], aV[2]);
+      aV[3] = du_mfma(xv[st].w, bopB[st], aV[3]);
       if ((st & 1) == 1 && st < 15) epi(1 + (st >> 1), SL ^ 1, yP, cwP);
     }
-    if (ROLE == 0) {
+    TR_DUO_MARK(2);
+    // T of sample k -> U partial of this unit -> Z partial (16 classes) -> LDS
+    const du_f32x4 T = (aT[0] + aT[1]) + (aT[2] + aT[3]);
+    TP = T;
 #pragma unroll
-      for (int rb = 0; rb < nrb; ++rb) {
-        const du_f32x4 T = (acc[rb][0] + acc[rb][1]) + (acc[rb][2] + acc[rb][3]);
-        accP[rb][0] = T;
-        float u = phiU[rb][0] * T.x;
-        u = fmaf(phiU[rb][1], T.y, u);
-        u = fmaf(phiU[rb][2], T.z, u);
-        u = fmaf(phiU[rb][3], T.w, u);
-        u += du_dpp<0x124>(u);  // row_ror:4
-        u += du_dpp<0x128>(u);  // row_ror:8
-        u = du_xor16_sum(u);
-        u = du_xor32_sum(u);
-        uP[rb][0] = du_rdl(u, 0);
-        uP[rb][1] = du_rdl(u, 1);
-        uP[rb][2] = du_rdl(u, 2);
-        uP[rb][3] = du_rdl(u, 3);
-        float zpart = wpc[rb][0] * uP[rb][0];
-        zpart = fmaf(wpc[rb][1], uP[rb][1], zpart);
-        zpart = fmaf(wpc[rb][2], uP[rb][2], zpart);
-        zpart = fmaf(wpc[rb][3], uP[rb][3], zpart);
-        // every row holds the same 16 class partials: all four rows store (same value, same slot)
-        sZ[(SL * 16 + c) * 4 + rb + nrb * s] = zpart;
-      }
-    } else {
-#pragma unroll
-      for (int rb = 0; rb < 2; ++rb)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) accP[rb][q] = acc[rb][q];
-    }
+    for (int q = 0; q < 4; ++q) VP[q] = aV[q];
+    float u = phiU[0] * T.x;
+    u = fmaf(phiU[1], T.y, u);
+    u = fmaf(phiU[2], T.z, u);
+    u = fmaf(phiU[3], T.w, u);
+    u += du_dpp<0x124>(u);  // row_ror:4
+    u += du_dpp<0x128>(u);  // row_ror:8
+    u = du_xor16_sum(u);
+    u = du_xor32_sum(u);
+    uP[0] = du_rdl(u, 0);
+    uP[1] = du_rdl(u, 1);
+    uP[2] = du_rdl(u, 2);
+    uP[3] = du_rdl(u, 3);
+    float zpart = wpc[0] * uP[0];
+    zpart = fmaf(wpc[1], uP[1], zpart);
+    zpart = fmaf(wpc[2], uP[2], zpart);
+    zpart = fmaf(wpc[3], uP[3], zpart);
+    // every row holds the same 16 class partials: all four rows store (same value, same slot)
+    sZ[(SL * 16 + c) * 4 + rb + 2 * s] = zpart;
     yP = yC;
     cwP = cwC;
+    if (EARLY) {
+      // every wave is past the GEMM of k: slot SL takes sample k + 2 now, one wait + barrier
+      // earlier than the slot-free point of the interleaved scheme (a dummy refill of the last
+      // sample when there is none: vmcnt counts stay fixed)
+      du_barrier();
+      dma_sample(src_of(k + 2 < nr ? k + 2 : nr - 1), SL);
+    }
+    TR_DUO_MARK(3);
   };
   for (int k = 0; k < nr; k += 2) {
     iter(std::integral_constant<int, 0>(), k);
     if (k + 1 < nr) iter(std::integral_constant<int, 1>(), k + 1);
   }
+#if TR_DUO_PROFILE
+  if (lane == 0 && blockIdx.x < 512)
+    for (int q = 0; q < 4; ++q) g_duo_prof[blockIdx.x][wv][q] = prof[q];
+#endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last (harmless) refill has landed
   du_barrier();  // Z partials of the last sample
   if (nr > 0) {
@@ -413,54 +423,41 @@ __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, cons
     for (int st = 0; st < 8; ++st) epi(st, (nr - 1) & 1, yP, cwP);
   }
 
-  // ---- fixed-order reduction into an LDS image of the arena (k_mnl_fused's unit order), slab ----
-  if (ROLE == 1) {  // fold the four row classes (lanes l, l^16, l^32, l^48)
+  // ---- fixed-order reduction into an LDS image of the arena (wave order), slab ----
 #pragma unroll
-    for (int rb = 0; rb < 2; ++rb)
+  for (int q = 0; q < 4; ++q)  // fold the V unit's four row classes (lanes l, l^16, l^32, l^48)
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          float x = gacc[rb][q][v];
-          x += __shfl_xor(x, 16, TR_WAVE);
-          x += __shfl_xor(x, 32, TR_WAVE);
-          gacc[rb][q][v] = x;
-        }
-  }
+    for (int v = 0; v < 4; ++v) {
+      float x = gV[q][v];
+      x += __shfl_xor(x, 16, TR_WAVE);
+      x += __shfl_xor(x, 32, TR_WAVE);
+      gV[q][v] = x;
+    }
   float* sG = lds + g.du_oG;
   __syncthreads();
   for (int64_t e = t; e < g.slab; e += DU_T) sG[e] = 0.f;
   __syncthreads();
-  // unit order of k_mnl_fused: A-units by (ib, jb, rb), then B-units by (jb, ib, rb)
   for (int ws = 0; ws < DU_NW; ++ws) {
     if (ws == wv) {
 #pragma unroll
-      for (int rb = 0; rb < 2; ++rb) {
-        if (rb >= nrb) continue;
-        const int rq = 4 * rb + l3;
-        const bool rqv = rq < R;
-        if (ROLE == 0) {
+      for (int v = 0; v < 4; ++v) {
+        const int row = 64 * ib + 4 * (lane >> 2) + v;
+        if (rqv) sG[row * R + rq] += gT[v];
+      }
+      if (cok && rg < R) sG[g.offPC + c * R + rg] += dpc;
+      if (lane < 16 && rqv) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
 #pragma unroll
           for (int v = 0; v < 4; ++v) {
-            const int row = 64 * ib + 4 * (lane >> 2) + v;
-            if (row < I && rqv) sG[row * R + rq] += gacc[rb][0][v];
+            const int j = 64 * jb + 16 * (lane >> 2) + 4 * v + q;
+            sG[g.offP1 + j * R + rq] += gV[q][v];
           }
-          const int r = 4 * rb + grow;
-          if (cok && r < R) sG[g.offPC + c * R + r] += dpc[rb];
-        } else if (lane < 16 && rqv) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-#pragma unroll
-            for (int v = 0; v < 4; ++v) {
-              const int j = 64 * jb + 16 * (lane >> 2) + 4 * v + q;
-              if (j < J) sG[g.offP1 + j * R + rq] += gacc[rb][q][v];
-            }
-        }
       }
     }
     __syncthreads();
   }
-  if (ROLE == 0 && wv == 0) {
+  if (wv == 0) {
     lsum = tr_wave_allreduce_d(lsum);
     if (lane == 0) {
       a.dpart[2 * blockIdx.x] = lsum;
@@ -471,26 +468,21 @@ __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, cons
   for (int64_t e = t; e < g.slab; e += DU_T) slab[e] = sG[e];
 }
 
-template <int NRB, int JT>
+template <int JT>
 __global__ __launch_bounds__(DU_T, 2) void k_mnl_duo(MnlGeom g, DuArgs a, const int64_t* __restrict__ lab,
                                                   const float* __restrict__ class_w, const int32_t* __restrict__ stop) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   if (stop != nullptr && *stop != 0) return;
   const int lane = threadIdx.x & (TR_WAVE - 1);
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / TR_WAVE);
-  if (wv < 2)
-    duo_body<0, NRB, JT>(g, a, lab, class_w, lds, wv, lane);
-  else
-    duo_body<1, NRB, JT>(g, a, lab, class_w, lds, wv, lane);
+  duo_body<JT>(g, a, lab, class_w, lds, wv, lane);
 }
 
 // ------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------
 static const void* duo_kernel(const MnlGeom& g) {
-  if (g.J == 64)
-    return g.nrb == 2 ? reinterpret_cast<const void*>(&k_mnl_duo<2, 64>) : reinterpret_cast<const void*>(&k_mnl_duo<1, 64>);
-  return g.nrb == 2 ? reinterpret_cast<const void*>(&k_mnl_duo<2, 128>) : reinterpret_cast<const void*>(&k_mnl_duo<1, 128>);
+  return g.J == 64 ? reinterpret_cast<const void*>(&k_mnl_duo<64>) : reinterpret_cast<const void*>(&k_mnl_duo<128>);
 }
 
 void mnl_duo_geom(MnlGeom* g) {
@@ -499,14 +491,14 @@ void mnl_duo_geom(MnlGeom* g) {
   if (env != nullptr && env[0] == '0') return;
   // compiled shapes: a 32 KiB sample as (128, 64) or (64, 128) (two 64-row blocks, 8 LDS-DMA
   // groups per wave, chunk swizzle q ^ (i & 15))
-  if (!g->full || g->I * g->J != 8192 || (g->J != 64 && g->J != 128) || g->nrb > 2 || g->C > kMnlCMax) return;
+  if (!g->full || g->I * g->J != 8192 || (g->J != 64 && g->J != 128) || g->nrb != 2 || g->C > kMnlCMax) return;
   if (g->smask != 15) return;
   const int64_t spf = (int64_t)g->I * g->J;
   int64_t o = 2 * spf;  // ring of two samples
   g->du_oZ = (int)o;
   o += 2 * 16 * 4;
   g->du_oP1 = (int)o;
-  o += (int64_t)g->Rp * (g->J + 4);
+  o += 8LL * (g->J + 4);
   o = (o + 3) & ~(int64_t)3;
   g->du_oG = g->slab <= 2 * spf ? 0 : (int)o;  // the arena image aliases the drained ring
   if (g->du_oG) o += g->slab;
@@ -538,20 +530,17 @@ hipError_t launch_mnl_duo(const MnlGeom& g, int grid, const float* X, int64_t N,
   if (grid < 1 || rows_per_wg < 0 || xld % 4 != 0 || (int64_t)grid * rows_per_wg < N) return hipErrorInvalidValue;
   DuArgs a{X, N, xld, phi, w, scale, gpart, dpart, rows_per_wg, reverse};
   const size_t lds = (size_t)g.du_lds_floats * 4;
-#define TR_DUO_LAUNCH(NRB, JT) hipLaunchKernelGGL((k_mnl_duo<NRB, JT>), dim3(grid), dim3(DU_T), lds, st, g, a, lab, class_w, stop)
-  if (g.J == 64) {
-    if (g.nrb == 2)
-      TR_DUO_LAUNCH(2, 64);
-    else
-      TR_DUO_LAUNCH(1, 64);
-  } else {
-    if (g.nrb == 2)
-      TR_DUO_LAUNCH(2, 128);
-    else
-      TR_DUO_LAUNCH(1, 128);
-  }
-#undef TR_DUO_LAUNCH
+if (g.J == 64)
+    hipLaunchKernelGGL((k_mnl_duo<64>), dim3(grid), dim3(DU_T), lds, st, g, a, lab, class_w, stop);
+  else
+    hipLaunchKernelGGL((k_mnl_duo<128>), dim3(grid), dim3(DU_T), lds, st, g, a, lab, class_w, stop);
   return hipGetLastError();
 }
 
 }  // namespace tr
+
+#if TR_DUO_PROFILE
+extern "C" int tr_duo_profile_read(unsigned long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_duo_prof), sizeof(g_duo_prof));
+}
+#endif
