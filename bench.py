@@ -285,7 +285,7 @@ def main():
     elif kt["stream_fused"][1] and "mnl-fused-1pass" in plan.describe:
         dom = "stream_fused"
         bytes_launch = N * P * 4 + N * 8  # X row + int64 label per sample
-        dom_name = "k_mnl_fused"
+        dom_name = "k_mnl_duo" if " duo " in plan.describe else "k_mnl_fused"
     elif kt["stream_fused"][1]:
         dom = "stream_fused"
         bytes_launch = N * P * 4 + N * 4

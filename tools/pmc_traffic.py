@@ -15,7 +15,7 @@ import json
 import os
 import re
 
-KERNELS = {"k_linear_fused": r"k_linear_fused", "k_linear_cluster": r"k_linear_cluster", "k_mnl_fused": r"k_mnl_fused", "k_rows": r"k_rows<", "k_rows_mfma": r"k_rows_mfma<", "k_cols": r"k_cols<",
+KERNELS = {"k_linear_fused": r"k_linear_fused", "k_linear_cluster": r"k_linear_cluster", "k_mnl_fused": r"k_mnl_fused", "k_mnl_duo": r"k_mnl_duo", "k_rows": r"k_rows<", "k_rows_mfma": r"k_rows_mfma<", "k_cols": r"k_cols<",
            "k_reduce_slabs": r"k_reduce_slabs", "k_mttkrp": r"k_mttkrp", "k_update": r"k_update",
            "k_spec_fused": r"k_spec_fused<0", "k_spec_slice": r"k_spec_slice", "k_spec_prep": r"k_spec_prep", "k_spec_chain": r"k_spec_chain"}
 

@@ -13,7 +13,7 @@ cd /tmp || exit 1
 for cfg in "$@"; do
   case $cfg in
     c2) alg=8590196736; dom=k_linear_fused ;;
-    c3) alg=2148007936; dom=k_mnl_fused ;;
+    c3) alg=2148007936; dom=k_mnl_duo ;;
     c4) alg=8590000128; dom=k_linear_cluster ;;
     c5) alg=4328783872; dom=k_spec_slice ;;
     *) alg=""; dom=k_linear_fused ;;
@@ -39,7 +39,7 @@ for cfg in "$@"; do
         -d $OUT/mfma -o $cfg -- python $ROOT/bench.py --config $cfg --steps 10 --warmup 2 --no-cpu-baseline \
         > /dev/null 2> $OUT/${cfg}_mfma.err || exit 1
     # algorithmic flops per launch: c3 factored pass 4*P*R per sample; c5 4*W*D*(n_out + Rs*Cc) per sample
-    case $cfg in c3) fl=17179869184; kre="k_mnl_fused" ;; c5) fl=77913391104; kre="k_spec_slice" ;; esac
+    case $cfg in c3) fl=17179869184; kre="k_mnl_duo" ;; c5) fl=77913391104; kre="k_spec_slice" ;; esac
     python $ROOT/tools/pmc_mfma.py --config $cfg --csv $(ls $OUT/mfma/${cfg}*counter_collection.csv | tail -1) \
         --kernel "$kre" --flops $fl --out $OUT/${cfg}_mfma.json || exit 1
   fi
