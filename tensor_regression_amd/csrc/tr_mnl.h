@@ -40,7 +40,7 @@ struct MnlGeom {
   // two-workgroups-per-CU variant (tr_mnl_duo.hip): 4 waves, each owning every rank block of
   // one (i, j) block; LDS carve of ONE workgroup (floats)
   int duo;
-  int du_oZ, du_oP1, du_oG, du_lds_floats;
+  int du_oZ, du_oP1, du_oG, du_oPF, du_lds_floats;
 };
 
 // Fills g; false (with a reason) when the shape is outside the kernel's envelope.

@@ -51,7 +51,7 @@ namespace {
 constexpr int DU_NW = 4;
 constexpr int DU_T = DU_NW * TR_WAVE;
 #ifndef TR_DUO_XL
-#define TR_DUO_XL 8
+#define TR_DUO_XL 6
 #endif
 constexpr int XL = TR_DUO_XL;  // GEMM steps an operand quad is read ahead of its MFMAs (B-waves)
 #ifndef TR_DUO_DMA_EVERY
@@ -69,6 +69,26 @@ constexpr bool EARLY = TR_DUO_EARLY != 0;
 #define TR_DUO_XLA 4
 #endif
 constexpr int XLA = TR_DUO_XLA;  // the same for the A-waves (X and Phi1 quads)
+#ifndef TR_DUO_SB
+#define TR_DUO_SB 1
+#endif
+// 1: a scheduling fence after every GEMM step, so the operand reads stay XL / XLA steps ahead of
+// their MFMAs (left alone, the scheduler issues the T unit's reads one step ahead and waits on
+// them: exposed LDS latency in every step) and the epilogue stages stay between the steps
+constexpr bool SB = TR_DUO_SB != 0;
+#ifndef TR_DUO_PF
+#define TR_DUO_PF 0
+#endif
+#ifndef TR_DUO_IL
+#define TR_DUO_IL 0
+#endif
+// 1: workgroup b takes samples b, b + grid, b + 2 grid, ... (the chip streams one contiguous
+// front of X); 0: a contiguous range of rows_per_wg samples per workgroup
+constexpr bool IL = TR_DUO_IL != 0;
+// > 0: every lane of the workgroup pulls one 128-B line of sample k + PF into L2 during the GEMM
+// of k (one dword LDS-DMA into a scratch line per wave), so the LDS-DMA of that sample one
+// iteration later meets L2 / MALL latency instead of a loaded HBM round trip; 0: no prefetch
+constexpr int PF = TR_DUO_PF;
 constexpr int DU_GMAX = 12;  // LDS-DMA pieces (1 KiB) per wave per sample (sample <= 48 KiB)
 typedef float du_f32x4 __attribute__((ext_vector_type(4)));
 
@@ -135,6 +155,16 @@ struct DuArgs {
   int64_t rows_per_wg;
   int reverse;
 };
+
+// L2 prefetch: one dword per lane from sbase + voff into the scratch LDS line at m0v (the value
+// is never read; only the line fill matters).  Counted by vmcnt like the LDS-DMA pieces.
+__device__ __forceinline__ void du_pf_s(uint32_t voff, const float* sbase, uint32_t m0v) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dword %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(sbase), "s"(m0v)
+               : "memory");
+}
 
 // One LDS-DMA piece per lane with a scalar base: 16 B from sbase + voff (bytes, per lane) to LDS
 // byte address m0v + 16 * lane.  No per-piece 64-bit address arithmetic; m0 is compiler-reserved
@@ -223,11 +253,15 @@ __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, cons
 #pragma unroll
   for (int m = 0; m < 4; ++m) boff[m] = (64 * ib + grow) * J + 64 * jb + 4 * (c ^ (4 * m + grow));
   const int pb = rq * P1S + 64 * jb;
+  // prefetch: lane (wv, lane) touches line 64 wv + lane of the sample (256 lines = 32 KiB)
+  const uint32_t pfoff = 128u * (uint32_t)(wv * TR_WAVE + lane);
+  const uint32_t pfm0 = lbase + 4u * (uint32_t)g.du_oPF;
 
-  const int64_t n0 = (int64_t)blockIdx.x * a.rows_per_wg;
-  const int64_t n1 = n0 + a.rows_per_wg < a.N ? n0 + a.rows_per_wg : a.N;
-  const int nr = (int)(n1 > n0 ? n1 - n0 : 0);
-  auto sample_of = [&](int k) -> int64_t { return a.reverse ? (n1 - 1 - k) : (n0 + k); };
+  const int64_t n0 = IL ? (int64_t)blockIdx.x : (int64_t)blockIdx.x * a.rows_per_wg;
+  const int64_t G = IL ? (int64_t)gridDim.x : 1;
+  const int64_t n1 = IL ? a.N : (n0 + a.rows_per_wg < a.N ? n0 + a.rows_per_wg : a.N);
+  const int nr = (int)(n1 > n0 ? (n1 - n0 + G - 1) / G : 0);
+  auto sample_of = [&](int k) -> int64_t { return n0 + G * (a.reverse ? (nr - 1 - k) : k); };
   auto src_of = [&](int k) -> const float* { return a.X + sample_of(k) * a.xld; };
 
   __syncthreads();
@@ -319,6 +353,7 @@ __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, cons
   if (nr > 0) {
     dma_sample(src_of(0), 0);
     if (EARLY) dma_sample(src_of(nr > 1 ? 1 : 0), 1);
+    if (!EARLY && PF > 0) du_pf_s(pfoff, src_of(nr > 1 ? 1 : 0), pfm0);  // keeps the loop's vmcnt(1) exact
   }
   int64_t yN = nr > 0 ? lab[sample_of(0)] : 0;  // label of the next GEMM sample (scalar, one ahead)
 
@@ -328,17 +363,23 @@ __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, cons
   // itself when k is the last one: a harmless refill of a free slot, no guard per piece)
   auto iter = [&](auto slot_c, int k) {
     constexpr int SL = decltype(slot_c)::value;
+    // the label of the next GEMM sample is a scalar load issued BEFORE the waits below: an SMEM
+    // load in flight (it may return out of order) would make every counted lgkmcnt wait of the
+    // GEMM's LDS reads a full lgkmcnt(0) drain; here the barrier's lgkmcnt(0) retires it while
+    // the wave waits for its LDS-DMA anyway
+    const int64_t yC = yN;
+    const bool more = k + 1 < nr;
+    yN = lab[sample_of(more ? k + 1 : k)];
     if (EARLY)  // own pieces of sample k (those of k + 1, issued after them, may be in flight)
       asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (PF > 0)  // every piece of k; the prefetch of k + PF - 1 (issued after them) may be in flight
+      asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     TR_DUO_MARK(0);
     du_barrier();  // everyone's pieces of k; Z partials of k - 1; slot SL ^ 1 free
     TR_DUO_MARK(1);
-    const int64_t yC = yN;
     const float cwC = du_rdl(cwl, (int)yC);
-    const bool more = k + 1 < nr;
-    yN = lab[sample_of(more ? k + 1 : k)];
     const float* psrc = (more && !(TR_DUO_SKIP & 1)) ? src_of(k + 1) : src_of(k);
     const uint32_t pm0 = lbase + (uint32_t)((SL ^ 1) * 4 * SPF) + (uint32_t)wv * 1024u;
     epi(0, SL ^ 1, yP, cwP);
@@ -363,6 +404,8 @@ __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, cons
       if (st + XL < 16) ldV(st + XL);
       if (!EARLY && st % DMA_EVERY == 0 && st / DMA_EVERY < 8)
         du_dma_s(goff[st / DMA_EVERY], psrc, pm0 + (uint32_t)(st / DMA_EVERY) * 4096u);
+      if (!EARLY && PF > 0 && st == 8)
+        du_pf_s(pfoff, src_of(k + PF < nr ? k + PF : nr - 1), pfm0);
       aT[0] = du_mfma(xt[st].x, bq[st].x, aT[0]);
       aT[1] = du_mfma(xt[st].y, bq[st].y, aT[1]);
       aT[2] = du_mfma(xt[st].z, bq[st].z, aT[2]);
@@ -372,6 +415,7 @@ __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, cons
       aV[2] = du_mfma(xv[st].z, bopB[st], aV[2]);
       aV[3] = du_mfma(xv[st].w, bopB[st], aV[3]);
       if ((st & 1) == 1 && st < 15) epi(1 + (st >> 1), SL ^ 1, yP, cwP);
+      if (SB) __builtin_amdgcn_sched_barrier(0);
     }
     TR_DUO_MARK(2);
     // T of sample k -> U partial of this unit -> Z partial (16 classes) -> LDS
@@ -500,6 +544,8 @@ void mnl_duo_geom(MnlGeom* g) {
   g->du_oP1 = (int)o;
   o += 8LL * (g->J + 4);
   o = (o + 3) & ~(int64_t)3;
+  g->du_oPF = (int)o;  // prefetch scratch line (64 dwords, written by every wave, never read)
+  o += TR_WAVE;
   g->du_oG = g->slab <= 2 * spf ? 0 : (int)o;  // the arena image aliases the drained ring
   if (g->du_oG) o += g->slab;
   o = (o + 3) & ~(int64_t)3;
