@@ -748,8 +748,14 @@ __global__ __launch_bounds__(256) void k_cols(const float* __restrict__ X, int64
 
 // ==========================================================================================
 // K4: fixed-order slab reduction  out[col] = sum_k part[k][col]  (+ scalar partials)
-// Workgroup = 16 waves x 64 vector columns; wave q sums slabs q, q+16, q+32, ... (4 loads in
-// flight per lane); the 16 wave sums are combined in wave order through LDS (deterministic).
+// Summation order (fixed, the same for every launch shape): for q = 0..15 and j = 0..3,
+// a_j(q) = sum over rounds t of slab q + 16 j + 64 t (rounds while q + 64 t + 48 < nslabs; the
+// remaining slabs q + 64 T + 16 m go into a_0(q)); s_q = (a_0 + a_1) + (a_2 + a_3); out =
+// s_0 + s_1 + ... + s_15 left to right.  Workgroup = 16 waves x 16 vector columns: lane
+// (c = lane & 15, j = lane >> 4) of wave q forms a_j(q) of column c, its loads issued four at a
+// time ahead of the in-order adds (one memory round trip per four rounds: with 64 columns per
+// workgroup and one wave per q, few workgroups walked the slabs in dependent rounds); wave 0
+// then combines the 64 partials of a column through LDS in the order above.
 // Block 0 also reduces the per-wave/per-WG fp64 scalar partials (loss, bias gradient) and
 // writes them into the gradient arena.
 // ==========================================================================================
@@ -765,43 +771,51 @@ __global__ __launch_bounds__(1024) void k_reduce_slabs(const float* __restrict__
                                                        const int32_t* __restrict__ stop) {
   using V = VecT<W>;
   using VT = typename V::T;
-  constexpr int NWV = 16;
-  __shared__ VT sred[NWV][TR_WAVE];
+  constexpr int NWV = 16, CPW = 16, NP = 64;
+  __shared__ VT sred[NP][CPW];  // [4 q + j][column]
   __shared__ double dred[2][NWV];
   if (stop != nullptr && *stop != 0) return;
   const int lane = threadIdx.x & (TR_WAVE - 1);
   const int q = threadIdx.x / TR_WAVE;
+  const int c = lane & (CPW - 1), j = lane >> 4;
   const int64_t NCW = ncols / W;
-  const int64_t colv = (int64_t)blockIdx.x * TR_WAVE + lane;
+  const int64_t colv = (int64_t)blockIdx.x * CPW + c;
   const VT* pv = reinterpret_cast<const VT*>(part);
-  if (colv < NCW) {
-    VT a0 = V::zero(), a1 = V::zero(), a2 = V::zero(), a3 = V::zero();
-    int64_t k = q;
-    for (; k + 3 * NWV < nslabs; k += 4 * NWV) {
-      const VT u0 = pv[k * NCW + colv];
-      const VT u1 = pv[(k + NWV) * NCW + colv];
-      const VT u2 = pv[(k + 2 * NWV) * NCW + colv];
-      const VT u3 = pv[(k + 3 * NWV) * NCW + colv];
-      a0 = V::add(a0, u0);
-      a1 = V::add(a1, u1);
-      a2 = V::add(a2, u2);
-      a3 = V::add(a3, u3);
+  {
+    VT a = V::zero();
+    if (colv < NCW) {
+      int64_t T = nslabs > q + 48 ? (nslabs - q - 48 + NP - 1) / NP : 0;  // rounds
+      const VT* src = pv + (int64_t)(q + 16 * j) * NCW + colv;
+      const int64_t st = (int64_t)NP * NCW;
+      int64_t t = 0;
+      for (; t + 4 <= T; t += 4) {
+        const VT u0 = src[t * st], u1 = src[(t + 1) * st], u2 = src[(t + 2) * st], u3 = src[(t + 3) * st];
+        a = V::add(a, u0);
+        a = V::add(a, u1);
+        a = V::add(a, u2);
+        a = V::add(a, u3);
+      }
+      for (; t < T; ++t) a = V::add(a, src[t * st]);
+      if (j == 0)
+        for (int64_t k = q + NP * T; k < nslabs; k += NWV) a = V::add(a, pv[k * NCW + colv]);
     }
-    for (; k < nslabs; k += NWV) a0 = V::add(a0, pv[k * NCW + colv]);
-    sred[q][lane] = V::add(V::add(a0, a1), V::add(a2, a3));
+    sred[4 * q + j][c] = a;
   }
   __syncthreads();
-  if (q == 0 && colv < NCW) {
-    VT s = sred[0][lane];
+  if (q == 0 && j == 0 && colv < NCW) {
+    VT s = V::zero();
 #pragma unroll
-    for (int w = 1; w < NWV; ++w) s = V::add(s, sred[w][lane]);
+    for (int qq = 0; qq < NWV; ++qq) {
+      const VT sq = V::add(V::add(sred[4 * qq][c], sred[4 * qq + 1][c]), V::add(sred[4 * qq + 2][c], sred[4 * qq + 3][c]));
+      s = qq == 0 ? sq : V::add(s, sq);
+    }
     reinterpret_cast<VT*>(out)[colv] = s;
     if (chain_out != nullptr) {  // softplus chain of arena-layout slabs (k_spec_chain) fused
       const float* sv = reinterpret_cast<const float*>(&s);
 #pragma unroll
-      for (int c = 0; c < W; ++c) {
-        const int64_t e = colv * W + c;
-        if (e < nchain) chain_out[e] = sv[c] * chain_dphi[e];
+      for (int cc = 0; cc < W; ++cc) {
+        const int64_t e = colv * W + cc;
+        if (e < nchain) chain_out[e] = sv[cc] * chain_dphi[e];
       }
     }
   }
@@ -1461,7 +1475,7 @@ hipError_t launch_reduce_slabs(int W, const float* part, int64_t nslabs, int64_t
                                const double* dpart, int64_t nd, double loss_scale, float* loss_slot,
                                float* bias_slot, const int32_t* stop, hipStream_t st, const float* chain_dphi,
                                float* chain_out, int64_t nchain, const uint32_t* err) {
-  const unsigned grid = cdiv(ncols / W, TR_WAVE);
+  const unsigned grid = cdiv(ncols / W, 16);
   if (W == 4)
     hipLaunchKernelGGL(k_reduce_slabs<4>, dim3(grid), dim3(1024), 0, st, part, nslabs, ncols, out, dpart, nd,
                        loss_scale, loss_slot, bias_slot, chain_dphi, chain_out, nchain, err, stop);
