@@ -748,18 +748,20 @@ __global__ __launch_bounds__(256) void k_cols(const float* __restrict__ X, int64
 
 // ==========================================================================================
 // K4: fixed-order slab reduction  out[col] = sum_k part[k][col]  (+ scalar partials)
-// Summation order (fixed, the same for every launch shape): for q = 0..15 and j = 0..3,
+// Summation order (fixed, the same for both layouts below): for q = 0..15 and j = 0..3,
 // a_j(q) = sum over rounds t of slab q + 16 j + 64 t (rounds while q + 64 t + 48 < nslabs; the
 // remaining slabs q + 64 T + 16 m go into a_0(q)); s_q = (a_0 + a_1) + (a_2 + a_3); out =
-// s_0 + s_1 + ... + s_15 left to right.  Workgroup = 16 waves x 16 vector columns: lane
-// (c = lane & 15, j = lane >> 4) of wave q forms a_j(q) of column c, its loads issued four at a
-// time ahead of the in-order adds (one memory round trip per four rounds: with 64 columns per
-// workgroup and one wave per q, few workgroups walked the slabs in dependent rounds); wave 0
-// then combines the 64 partials of a column through LDS in the order above.
-// Block 0 also reduces the per-wave/per-WG fp64 scalar partials (loss, bias gradient) and
-// writes them into the gradient arena.
+// s_0 + s_1 + ... + s_15 left to right.  Workgroup = 16 waves (q = wave).
+//   WIDE   (64 vector columns per workgroup): lane = column, the thread forms a_0..a_3 (4 loads
+//          in flight); for many columns (enough workgroups to fill the chip).
+//   NARROW (16 vector columns per workgroup): lane (c = lane & 15, j = lane >> 4) forms a_j(q)
+//          alone, its loads issued four rounds ahead of the in-order adds; for few columns and
+//          many slabs (config 3: 512 slabs of 1.6 K floats), where WIDE ran 7 workgroups
+//          through 8 dependent load rounds.
+// Both write bitwise-identical sums.  Block 0 also reduces the per-wave/per-WG fp64 scalar
+// partials (loss, bias gradient) and writes them into the gradient arena.
 // ==========================================================================================
-template <int W>
+template <int W, bool NARROW>
 __global__ __launch_bounds__(1024) void k_reduce_slabs(const float* __restrict__ part, int64_t nslabs,
                                                        int64_t ncols, float* __restrict__ out,
                                                        const double* __restrict__ dpart, int64_t nd,
@@ -771,22 +773,23 @@ __global__ __launch_bounds__(1024) void k_reduce_slabs(const float* __restrict__
                                                        const int32_t* __restrict__ stop) {
   using V = VecT<W>;
   using VT = typename V::T;
-  constexpr int NWV = 16, CPW = 16, NP = 64;
-  __shared__ VT sred[NP][CPW];  // [4 q + j][column]
+  constexpr int NWV = 16, NP = 64;
+  constexpr int CPW = NARROW ? 16 : TR_WAVE;  // vector columns per workgroup
+  __shared__ VT sred[NWV * TR_WAVE];          // NARROW: [4 q + j][c]; WIDE: [q][lane]
   __shared__ double dred[2][NWV];
   if (stop != nullptr && *stop != 0) return;
   const int lane = threadIdx.x & (TR_WAVE - 1);
   const int q = threadIdx.x / TR_WAVE;
-  const int c = lane & (CPW - 1), j = lane >> 4;
+  const int c = lane & (CPW - 1), j = NARROW ? lane >> 4 : 0;
   const int64_t NCW = ncols / W;
   const int64_t colv = (int64_t)blockIdx.x * CPW + c;
   const VT* pv = reinterpret_cast<const VT*>(part);
-  {
+  const int64_t T = nslabs > q + 48 ? (nslabs - q - 48 + NP - 1) / NP : 0;  // full rounds of wave q
+  const int64_t st = (int64_t)NP * NCW;
+  if (NARROW) {
     VT a = V::zero();
     if (colv < NCW) {
-      int64_t T = nslabs > q + 48 ? (nslabs - q - 48 + NP - 1) / NP : 0;  // rounds
       const VT* src = pv + (int64_t)(q + 16 * j) * NCW + colv;
-      const int64_t st = (int64_t)NP * NCW;
       int64_t t = 0;
       for (; t + 4 <= T; t += 4) {
         const VT u0 = src[t * st], u1 = src[(t + 1) * st], u2 = src[(t + 2) * st], u3 = src[(t + 3) * st];
@@ -799,14 +802,31 @@ __global__ __launch_bounds__(1024) void k_reduce_slabs(const float* __restrict__
       if (j == 0)
         for (int64_t k = q + NP * T; k < nslabs; k += NWV) a = V::add(a, pv[k * NCW + colv]);
     }
-    sred[4 * q + j][c] = a;
+    sred[(4 * q + j) * CPW + c] = a;
+  } else if (colv < NCW) {
+    VT a0 = V::zero(), a1 = V::zero(), a2 = V::zero(), a3 = V::zero();
+    const VT* src = pv + (int64_t)q * NCW + colv;
+    for (int64_t t = 0; t < T; ++t) {
+      const VT u0 = src[t * st];
+      const VT u1 = src[t * st + 16 * NCW];
+      const VT u2 = src[t * st + 32 * NCW];
+      const VT u3 = src[t * st + 48 * NCW];
+      a0 = V::add(a0, u0);
+      a1 = V::add(a1, u1);
+      a2 = V::add(a2, u2);
+      a3 = V::add(a3, u3);
+    }
+    for (int64_t k = q + NP * T; k < nslabs; k += NWV) a0 = V::add(a0, pv[k * NCW + colv]);
+    sred[q * TR_WAVE + lane] = V::add(V::add(a0, a1), V::add(a2, a3));
   }
   __syncthreads();
   if (q == 0 && j == 0 && colv < NCW) {
     VT s = V::zero();
 #pragma unroll
     for (int qq = 0; qq < NWV; ++qq) {
-      const VT sq = V::add(V::add(sred[4 * qq][c], sred[4 * qq + 1][c]), V::add(sred[4 * qq + 2][c], sred[4 * qq + 3][c]));
+      const VT sq = NARROW ? V::add(V::add(sred[(4 * qq) * CPW + c], sred[(4 * qq + 1) * CPW + c]),
+                                    V::add(sred[(4 * qq + 2) * CPW + c], sred[(4 * qq + 3) * CPW + c]))
+                           : sred[qq * TR_WAVE + lane];
       s = qq == 0 ? sq : V::add(s, sq);
     }
     reinterpret_cast<VT*>(out)[colv] = s;
@@ -1475,13 +1495,23 @@ hipError_t launch_reduce_slabs(int W, const float* part, int64_t nslabs, int64_t
                                const double* dpart, int64_t nd, double loss_scale, float* loss_slot,
                                float* bias_slot, const int32_t* stop, hipStream_t st, const float* chain_dphi,
                                float* chain_out, int64_t nchain, const uint32_t* err) {
-  const unsigned grid = cdiv(ncols / W, 16);
-  if (W == 4)
-    hipLaunchKernelGGL(k_reduce_slabs<4>, dim3(grid), dim3(1024), 0, st, part, nslabs, ncols, out, dpart, nd,
-                       loss_scale, loss_slot, bias_slot, chain_dphi, chain_out, nchain, err, stop);
-  else
-    hipLaunchKernelGGL(k_reduce_slabs<1>, dim3(grid), dim3(1024), 0, st, part, nslabs, ncols, out, dpart, nd,
-                       loss_scale, loss_slot, bias_slot, chain_dphi, chain_out, nchain, err, stop);
+  // NARROW when the wide layout would leave most CUs idle (fewer than 128 workgroups)
+  const bool narrow = cdiv(ncols / W, TR_WAVE) < 128;
+  const unsigned grid = cdiv(ncols / W, narrow ? 16 : TR_WAVE);
+#define TR_RED(WW, NN)                                                                                      \
+  hipLaunchKernelGGL((k_reduce_slabs<WW, NN>), dim3(grid), dim3(1024), 0, st, part, nslabs, ncols, out, dpart, \
+                     nd, loss_scale, loss_slot, bias_slot, chain_dphi, chain_out, nchain, err, stop)
+  if (W == 4) {
+    if (narrow)
+      TR_RED(4, true);
+    else
+      TR_RED(4, false);
+  } else if (narrow) {
+    TR_RED(1, true);
+  } else {
+    TR_RED(1, false);
+  }
+#undef TR_RED
   return hipGetLastError();
 }
 
