@@ -19,11 +19,11 @@ for cfg in "$@"; do
     *) alg=""; dom=k_linear_fused ;;
   esac
   echo "[$cfg] bench" >&2
-  timeout -k 10 300 python $ROOT/bench.py --config $cfg --steps 30 --warmup 5 \
+  timeout -k 10 300 python $ROOT/bench.py --config $cfg --steps 30 --warmup 200 \
       > $OUT/${cfg}_bench.json 2> $OUT/${cfg}_bench.err || exit 1
   echo "[$cfg] kernel trace" >&2
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o $cfg -- \
-      python $ROOT/bench.py --config $cfg --steps 30 --warmup 5 --no-cpu-baseline \
+      python $ROOT/bench.py --config $cfg --steps 30 --warmup 200 --no-cpu-baseline \
       > $OUT/${cfg}_bench_under_rocprof.json 2> $OUT/${cfg}_trace.err || exit 1
   echo "[$cfg] pmc FETCH_SIZE" >&2
   timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $OUT/fetch -o $cfg -- \
