@@ -54,6 +54,12 @@ CONFIGS["c6"] = dict(kind="linear", rows=65536, dims=(256, 128), rank=8, windowe
                      workload="windowed variant of configs[1] (util.py:67-114 WindowedDataset): 65536 windows of "
                               "256 x 128 over an untiled (65791, 128) fp32 series, read in place through the row "
                               "stride (no materialised windows), rank 8, Adam lr 0.01")
+CONFIGS["c7"] = dict(kind="linear", rows=65536, dims=(256, 128), rank=8, hoststream=True, chunk_rows=8192,
+                     expect="fused-1pass", default_warmup=3,
+                     workload="out-of-core variant of configs[1] (util.py HostStream): X (65536, 256, 128) fp32 in "
+                              "pinned host memory, streamed through two 1 GiB HBM buffers in 8 chunks of 8192 "
+                              "samples every iteration (copies on their own stream, double-buffered against the "
+                              "kernels), rank 8, Adam lr 0.01")
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32 = the fp32 vector rate
 
 
@@ -154,23 +160,85 @@ def cpu_baseline(cfg, X, y, model_init, budget_s=15.0, threads=None):
     t1 = time.perf_counter()
     per = max((t1 - t0) / 2, 1e-3)
     iters = int(max(5, min(200, budget_s / per)))
-    log(f"cpu baseline: {nthreads} threads, {per:.2f} s/iteration, timing {iters} iterations")
-    el = 0.0
-    done = 0
-    while done < iters:  # chunks of <= 5 iterations, a progress line after each (long configs)
-        k = min(5, iters - done)
+    log(f"cpu baseline: {nthreads} threads, {per:.2f} s/iteration, timing {iters} iterations one by one")
+    times = []
+    load0 = os.getloadavg()
+    for k in range(iters):  # each timed alone: one fit_Adam iteration (the op sequence of every later one)
         t0 = time.perf_counter()
-        run(k)
-        el += time.perf_counter() - t0
-        done += k
-        log(f"cpu baseline: {done}/{iters} iterations, {el:.1f} s")
+        run(1)
+        times.append(time.perf_counter() - t0)
+        if k % 5 == 4 or k == iters - 1:
+            log(f"cpu baseline: {k + 1}/{iters} iterations, {sum(times):.1f} s")
+    load1 = os.getloadavg()
+    t = np.array(times)
+    med, lo, hi = float(np.median(t)), float(t.min()), float(t.max())
+    spread = hi / lo
     N = X.shape[0]
-    return {"value": N * iters / el, "unit": "samples/s", "cores": torch.get_num_threads(), "kind": "port",
+    note = (f"; per-iteration spread {spread:.1f}x > 2x: the host is shared (load average {load0[0]:.0f} -> "
+            f"{load1[0]:.0f} on {info['os_cpu_count']} CPUs), the median is the reported value"
+            if spread > 2.0 else "")
+    return {"value": N / med, "unit": "samples/s", "cores": torch.get_num_threads(), "kind": "port",
             "sample": f"oracle/cp_oracle.py fit_Adam (torch {torch.__version__} CPU, the reference's op order) on "
-                      f"the same {N} x {list(cfg['dims'])} X (full per-GPU size), {iters} timed iterations after 2 "
-                      f"warm-up ({el:.1f} s), torch.set_num_threads({nthreads}) "
-                      f"({'OMP_NUM_THREADS quota of this job' if threads is None and quota else 'threads'})",
-            "host": info, "ms_per_step": 1e3 * el / iters}
+                      f"the same {N} x {list(cfg['dims'])} X (full per-GPU size): {iters} iterations each timed "
+                      f"alone after 2 warm-up ({t.sum():.1f} s), value = N / median iteration time, "
+                      f"torch.set_num_threads({nthreads}) "
+                      f"({'OMP_NUM_THREADS quota of this job' if threads is None and quota else 'threads'})" + note,
+            "iteration_s": {"median": med, "min": lo, "max": hi, "spread_max_over_min": spread, "n": iters},
+            "samples_per_s_range": [N / hi, N / lo], "loadavg_1min": [load0[0], load1[0]],
+            "host": info, "ms_per_step": 1e3 * med}
+
+
+def host_stream_report(model, hs, Xres, y, fit, ms_step, dev):
+    """Out-of-core fit (util.HostStream): H2D rate of the streamed fit against this host's pinned
+    copy rate, and how much of the copy time the kernels hide.
+      copy_only_ms     every chunk of X copied through the two buffers, no kernels
+      compute_only_ms  the same fit step with X resident in HBM
+      overlap          (copy_only + compute_only - step) / min(copy_only, compute_only): 1 = the
+                       shorter of the two is completely hidden behind the longer."""
+    nbytes = hs.X.numel() * 4
+    torch.cuda.synchronize()
+    # pinned H2D peak: one 1 GiB copy from the same pinned X, best of 3
+    n = min(hs.X.numel(), 1 << 28)
+    dst = torch.empty(n, dtype=torch.float32, device=dev)
+    src = hs.X.reshape(-1)[:n]
+    best = float("inf")
+    for _ in range(3):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        dst.copy_(src, non_blocking=True)
+        e1.record()
+        e1.synchronize()
+        best = min(best, e0.elapsed_time(e1))
+    del dst
+    peak = n * 4 / (best * 1e-3) / 1e9
+    # copy only: the stream's own chunk loop with no kernels
+    reps = 3
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        for _c in hs.chunks():
+            pass
+    torch.cuda.synchronize()
+    copy_ms = 1e3 * (time.perf_counter() - t0) / reps
+    # compute only: the same model, X resident (a fresh plan for the resident rows)
+    state = [a.detach().clone() for a in model.Bcp], model.bias.detach().clone(), list(model.loss_running)
+    k = 20
+    model.fit_Adam(Xres, y, lambda_L2=0.01, max_iter=3, tol=0, patience=10, Adam_kwargs={"lr": 0.01})
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    model.fit_Adam(Xres, y, lambda_L2=0.01, max_iter=k, tol=0, patience=10, Adam_kwargs={"lr": 0.01})
+    torch.cuda.synchronize()
+    compute_ms = 1e3 * (time.perf_counter() - t0) / k
+    with torch.no_grad():
+        for a, b in zip(model.Bcp, state[0]):
+            a.copy_(b)
+        model.bias.copy_(state[1])
+    model.loss_running[:] = state[2]
+    h2d = nbytes / (ms_step * 1e-3) / 1e9
+    overlap = (copy_ms + compute_ms - ms_step) / min(copy_ms, compute_ms)
+    return {"h2d_GBps": h2d, "pinned_copy_peak_GBps": peak, "h2d_frac_of_peak": h2d / peak,
+            "copy_only_ms": copy_ms, "compute_only_ms": compute_ms, "step_ms": ms_step,
+            "overlap_hidden_frac": overlap, "chunk_rows": hs.chunk_rows, "bytes_per_step": nbytes}
 
 
 def main():
@@ -181,7 +249,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=200,
+    ap.add_argument("--warmup", type=int, default=None,
                     help="untimed fit_Adam iterations first: the compute-bound kernels (c3, c5) reach their "
                          "steady clock only after ~50 iterations (c3 kernel 0.402 ms after 5, 0.367 ms after 200)")
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
@@ -198,6 +266,8 @@ def main():
                     help="PMC traffic summary (tools/pmc_traffic.py output) for the roofline 'traffic' field")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
+    if args.warmup is None:  # 200 (< 0.5 s) resident; the PCIe-bound streamed config: 3 (0.5 s)
+        args.warmup = cfg.get("default_warmup", 200)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank_id = int(os.environ.get("RANK", "0"))
@@ -215,6 +285,10 @@ def main():
 
     X, y = make_data(cfg, rank_id, dev)
     torch.cuda.synchronize()
+    Xres = X  # the device-resident X (hoststream: for the copy / compute-only reference timings)
+    if cfg.get("hoststream"):
+        from tensor_regression_amd.util import HostStream
+        X = HostStream(X.cpu(), chunk_rows=cfg["chunk_rows"], device=dev)
     R = cfg["rank"]
     torch.manual_seed(1)
     if cfg["kind"] == "spectral":
@@ -278,6 +352,7 @@ def main():
     P = int(np.prod(cfg["dims"]))
     ms_step = 1e3 * el / args.steps
     value = world * N * args.steps / el
+    hoststream = host_stream_report(model, X, Xres, y, fit, ms_step, dev) if cfg.get("hoststream") else None
 
     if args.no_kernel_timing:
         if rank_id == 0:
@@ -296,7 +371,8 @@ def main():
         dom = "stream_fused"
         bytes_launch = N * P * 4 + N * 4 * cfg["n_out"]
         # algorithmic minimum: the lin term as a dense (W x D x n_out) contraction
-        # forward + backward, the spectral term's two GEMMs over Rs*Cc columns: 4*N*P*(n_out + Rs*Cc)
+        # forward + backward, the spectral term's two GEMMs over Rs*Cc columns (Cc = n_complex_dim + 1):
+        # 4*N*P*(n_out + Rs*Cc)
         flops_launch = 4 * N * P * (cfg["n_out"] + cfg["rank_spectral"] * (cfg["n_complex_dim"] + 1))
         dom_name = "k_spec_slice" if "slice-1pass" in plan.describe else "k_spec_fused"
     elif kt["stream_fused"][1] and "mnl-fused-1pass" in plan.describe:
@@ -306,6 +382,8 @@ def main():
     elif kt["stream_fused"][1]:
         dom = "stream_fused"
         bytes_launch = N * P * 4 + N * 4
+        if cfg.get("hoststream"):  # one launch per chunk
+            bytes_launch = bytes_launch // (kt["stream_fused"][1] // args.steps)
         if cfg.get("windowed"):
             # overlapping windows: the unique series (N + L - 1) x F is what must cross HBM; the
             # N * P window bytes are logical reads, mostly served by L2 / MALL
@@ -358,6 +436,9 @@ def main():
                      "kernel_avg_ms": dom_ms, "algorithmic_bytes_per_launch": bytes_launch},
         "kernel_avg_ms": kernel_avg,
     }
+    if hoststream is not None:
+        out["hoststream"] = hoststream
+        out["data"] += "; X resident in pinned host memory, copied to HBM every step (inside the timed region)"
     if flops_launch is not None:
         # spectral: the roofline time is the larger of the HBM time of the algorithmic bytes and
         # the fp32 matrix time of the algorithmic flops; at config 5 (18 flop/B < the 19.7 flop/B
@@ -379,7 +460,7 @@ def main():
         out["dtype"] = "fp32"
     if rank_id == 0 and world == 1 and not args.no_cpu_baseline:
         log("cpu baseline ...")
-        out["cpu_baseline"] = cpu_baseline(cfg, X, y, init, args.cpu_budget, args.cpu_threads)
+        out["cpu_baseline"] = cpu_baseline(cfg, Xres, y, init, args.cpu_budget, args.cpu_threads)
     else:
         out["cpu_baseline"] = None
     if rank_id == 0:

@@ -16,8 +16,10 @@
  * Conventions
  *   - Every pointer argument is DEVICE memory on the plan's device unless stated otherwise;
  *     the library never frees memory it did not allocate.
- *   - fp32 everywhere (the reference's multinomial class is fp32-only,
- *     multinomial_tensor_regression.py:255; the standard class defaults to fp32, :206).
+ *   - fp32 (the reference's multinomial and spectral classes are fp32-only,
+ *     multinomial_tensor_regression.py:255; the standard class defaults to fp32, :206), plus a
+ *     float64 linear model through the *_f64 entry points (CP_linear_regression(dtype=
+ *     torch.float64), standard_tensor_regression.py:206).
  *   - X is sample-major and C-contiguous: X[n, i_1, ..., i_K], i.e. an (N x P) row-major
  *     matrix with P = prod(dims).
  *   - Parameter arena: the Kruskal factor list `Bcp` packed back to back in the reference's
@@ -240,9 +242,17 @@ int tr_adam_step_f64(tr_plan* plan, double* params, const double* grad, double* 
  *                  weights = all rank_normal + rank_spectral weights
  *   tr_adam_step   also applies the spectral NaN stop (spectral…py:738-741): when the loss
  *                  is NaN and iter <= patience, *stop_flag = -(iter + 1) (stopped, not converged)
- * Envelope of the gfx950 kernel: n_w, n_d <= 256, n_out <= 256, Rn + Rs*n_complex <= 32, one
- * sample (n_w * n_d floats) plus scratch within the 160 KiB LDS of a CU; TR_E_UNSUPPORTED
- * otherwise.
+ * Envelope (tr_plan_create_spectral returns TR_E_UNSUPPORTED outside it, with the reason in
+ * tr_last_error()):  K = rank_normal + rank_spectral * n_complex <= 256, n_w <= 2^24,
+ * n_d, n_out <= 2^16, and one sample's epilogue — n_d * (K + 1) + (n_d + n_out) *
+ * (rank_normal + rank_spectral) floats (+ scratch) — within the 160 KiB LDS of a CU.  Inside it
+ * the plan picks (tr_plan_describe):
+ *   slice-1pass-mfma   training at n_w = 256, 97 <= n_d <= 130 (n_d >= 128 or n_d % 4 == 0),
+ *                      1 <= Rn <= 16, Rs * n_complex <= 16 with n_complex in {1, 2, 4},
+ *                      n_out <= 64 (and its LDS fits): column-slice single pass (config 5)
+ *   fused-1pass-mfma   K <= 32, n_w, n_d, n_out <= 256 and the whole sample + scratch in LDS:
+ *                      single pass; also every tr_forward / tr_spectral_latents of such a plan
+ *   generic-3kernel-mfma  any other shape in the envelope: T_n staged through HBM (three kernels)
  */
 int tr_plan_create_spectral(tr_plan** out, int device, int64_t n_w, int64_t n_d, int64_t n_out,
                             int rank_normal, int rank_spectral, int n_complex, int64_t max_rows,

@@ -458,6 +458,34 @@ def loss_grad_any(plan, X, target, class_weight, norm, arena, weights, grad, sto
             grad.add_(tmp)
 
 
+def collective_device(process_group):
+    """Device for the small host-logic collectives of a sharded fit: gloo takes CPU tensors, RCCL
+    ("nccl") the rank's current HIP device."""
+    import torch.distributed as dist
+    return "cpu" if dist.get_backend(process_group) == "gloo" else f"cuda:{torch.cuda.current_device()}"
+
+
+def agree(process_group, fn):
+    """Run this rank's local preparation `fn()` (argument checks, device copies, plan creation) and
+    make its failure collective: one MAX all-reduce of a failure flag, so if `fn` raised on any
+    rank every rank raises (the failing rank its own exception) and no rank is left blocked in a
+    later collective of the fit."""
+    import torch.distributed as dist
+    err, out = None, None
+    try:
+        out = fn()
+    except Exception as e:  # re-raised below, after the other ranks have been told
+        err = e
+    flag = torch.tensor([0 if err is None else 1], dtype=torch.int32, device=collective_device(process_group))
+    dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=process_group)
+    if err is not None:
+        raise err
+    if int(flag.item()):
+        raise RuntimeError("the sharded fit failed on another rank of the process group (see that rank's error); "
+                           "no rank started fitting")
+    return out
+
+
 def check_uniform(value, process_group, what, device):
     """Raise ValueError on EVERY rank when the ranks disagree on an integer (one all-reduce), so a
     mismatch cannot leave some ranks blocked in a later collective."""
@@ -466,16 +494,16 @@ def check_uniform(value, process_group, what, device):
     dist.all_reduce(n, op=dist.ReduceOp.MAX, group=process_group)
     if int(n[0]) != int(value) or -int(n[1]) != int(value):
         raise ValueError(f"ranks disagree on {what} (this rank {int(value)}, max {int(n[0])}, min {-int(n[1])}); "
-                         "a multinomial model's class count comes from its local labels: build every rank's model "
-                         "with the global class count (Bcp_init of the global shapes)")
+                         "every rank's model must have the same factor shapes")
 
 
 def sync_replicas(arena, process_group):
     """Start every rank's replica from the same parameters (multi-GPU fit_Adam).
 
-    The ranks must agree on the arena layout (for the multinomial model: the number of classes,
-    taken by the constructor from the local labels) — checked with one MIN/MAX all-reduce so a
-    mismatch raises on every rank instead of hanging in the per-iteration all-reduce — and then
+    The ranks must agree on the arena layout (a multinomial model takes the global class set
+    before this point, CP_logistic_regression._sync_class_set) — checked with one MIN/MAX
+    all-reduce so a mismatch raises on every rank instead of hanging in the per-iteration
+    all-reduce — and then
     take group rank 0's parameters (one broadcast per fit).  From there the replicas stay in
     lock-step: every rank applies the identical step to the bitwise-identical all-reduced sums."""
     import torch.distributed as dist

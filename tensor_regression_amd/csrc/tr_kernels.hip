@@ -516,21 +516,38 @@ __global__ __launch_bounds__(256) void k_rows_mfma(
   const bool cls_ok = i < C;
   // Bt is padded to 16 class rows (rows >= C are zero): unconditional loads, no per-lane branches
   const float4* br = reinterpret_cast<const float4*>(Bt + (int64_t)i * P + 8 * g);
-  tr_f32x4 acc[RT];
+  // Blocked summation: 8 independent accumulator chains per row tile (MFMA m of a step feeds
+  // chain m), folded by a fixed tree into a running total every 16 steps (512 features).  One
+  // chain over all P/4 MFMAs (round 2) left Z 6.5e-5 from exact at P = 8192, |Z| = 58
+  // (mnl_duo_t), 2x the probability error of the reference's own blocked fp32 GEMM; this order
+  // is 6.9e-6 (emulated).  Independent chains also keep back-to-back MFMAs independent.
+  tr_f32x4 ac[RT][8], acc[RT];
 #pragma unroll
-  for (int rt = 0; rt < RT; ++rt) acc[rt] = tr_f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int rt = 0; rt < RT; ++rt) {
+    acc[rt] = tr_f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int m = 0; m < 8; ++m) ac[rt][m] = tr_f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  auto fold = [&]() {
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      acc[rt] += ((ac[rt][0] + ac[rt][1]) + (ac[rt][2] + ac[rt][3])) + ((ac[rt][4] + ac[rt][5]) + (ac[rt][6] + ac[rt][7]));
+#pragma unroll
+      for (int m = 0; m < 8; ++m) ac[rt][m] = tr_f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
   const int nsteps = (int)(P / 32);
   auto step = [&](const float4(&xa)[RT], const float4(&xb)[RT], const float4 ba, const float4 bb) {
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
-      acc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[rt].x, ba.x, acc[rt], 0, 0, 0);
-      acc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[rt].y, ba.y, acc[rt], 0, 0, 0);
-      acc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[rt].z, ba.z, acc[rt], 0, 0, 0);
-      acc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[rt].w, ba.w, acc[rt], 0, 0, 0);
-      acc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(xb[rt].x, bb.x, acc[rt], 0, 0, 0);
-      acc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(xb[rt].y, bb.y, acc[rt], 0, 0, 0);
-      acc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(xb[rt].z, bb.z, acc[rt], 0, 0, 0);
-      acc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(xb[rt].w, bb.w, acc[rt], 0, 0, 0);
+      ac[rt][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[rt].x, ba.x, ac[rt][0], 0, 0, 0);
+      ac[rt][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[rt].y, ba.y, ac[rt][1], 0, 0, 0);
+      ac[rt][2] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[rt].z, ba.z, ac[rt][2], 0, 0, 0);
+      ac[rt][3] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[rt].w, ba.w, ac[rt][3], 0, 0, 0);
+      ac[rt][4] = __builtin_amdgcn_mfma_f32_16x16x4f32(xb[rt].x, bb.x, ac[rt][4], 0, 0, 0);
+      ac[rt][5] = __builtin_amdgcn_mfma_f32_16x16x4f32(xb[rt].y, bb.y, ac[rt][5], 0, 0, 0);
+      ac[rt][6] = __builtin_amdgcn_mfma_f32_16x16x4f32(xb[rt].z, bb.z, ac[rt][6], 0, 0, 0);
+      ac[rt][7] = __builtin_amdgcn_mfma_f32_16x16x4f32(xb[rt].w, bb.w, ac[rt][7], 0, 0, 0);
     }
   };
   int st = 0;
@@ -548,6 +565,7 @@ __global__ __launch_bounds__(256) void k_rows_mfma(
     __builtin_amdgcn_sched_barrier(0);  // keep all 4*RT+4 loads of the two steps in flight together
     step(xa0, xb0, ba0, bb0);
     step(xa1, xb1, ba1, bb1);
+    if (((st + 2) & 15) == 0) fold();
   }
   if (st < nsteps) {
     float4 xa0[RT], xb0[RT];
@@ -559,6 +577,7 @@ __global__ __launch_bounds__(256) void k_rows_mfma(
     const float4 ba0 = br[8 * st], bb0 = br[8 * st + 1];
     step(xa0, xb0, ba0, bb0);
   }
+  fold();
   const float NEG = -__builtin_huge_valf();
   double lsum = 0.0;
   if (MODE == MODE_MNL_LOGITS) {

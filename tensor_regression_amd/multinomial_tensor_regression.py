@@ -91,8 +91,11 @@ def model(X, Bcp, weights, non_negative, softplus_kwargs=None):
 class CP_logistic_regression():
     def __init__(self, X, y, rank=5, non_negative=False, weights=None, Bcp_init=None, Bcp_init_scale=1,
                  device='cpu', softplus_kwargs=None):
-        """(multinomial_tensor_regression.py:212-286; same arguments and attributes)."""
-        self.X = torch.as_tensor(X, dtype=torch.float32).to(device)
+        """(multinomial_tensor_regression.py:212-286; same arguments and attributes).  X may also
+        be a util.HostStream (host-resident X streamed through HBM every iteration; fit_Adam and
+        predict only)."""
+        from .util import HostStream
+        self.X = X if isinstance(X, HostStream) else torch.as_tensor(X, dtype=torch.float32).to(device)
         self.y = torch.as_tensor(y, dtype=torch.long).to(device)
         if weights is None:
             self.weights = torch.ones((rank), device=device)
@@ -112,6 +115,10 @@ class CP_logistic_regression():
             self.non_negative = non_negative
         self.n_classes = len(torch.unique(self.y))
         B_dims = np.concatenate((np.array(self.X.shape[1:]), [self.n_classes]))
+        # a class factor drawn here from the LOCAL labels may be widened to the global class set
+        # by a sharded fit_Adam (_sync_class_set); one passed in by the caller is never resized
+        self._class_factor_auto = Bcp_init is None
+        self._Bcp_init_scale = Bcp_init_scale
         if Bcp_init is None:
             self.Bcp = make_BcpInit(B_dims, self.rank, self.non_negative, scale=Bcp_init_scale, device=self.device)
         else:
@@ -125,10 +132,12 @@ class CP_logistic_regression():
 
     # ---- plumbing ------------------------------------------------------------------------------
     def _device_data(self):
-        dev = _engine.compute_device(self.X, self.device)
+        from .util import HostStream
+        hs = isinstance(self.X, HostStream)
+        dev = self.X.dev_index if hs else _engine.compute_device(self.X, self.device)
         c = self._dev_cache
         if c is None or c[0] != dev or c[1] is not self.X or c[2] is not self.y:
-            Xd = _engine.as_device_rows(self.X, dev)
+            Xd = self.X if hs else _engine.as_device_rows(self.X, dev)
             yd = self.y.to(f"cuda:{dev}", torch.long).contiguous()
             C = int(self.Bcp[-1].shape[0])
             ymin, ymax = int(yd.min().item()), int(yd.max().item())
@@ -138,6 +147,9 @@ class CP_logistic_regression():
         return self._dev_cache[0], self._dev_cache[3], self._dev_cache[4]
 
     def _get_plan(self, Xd, rows):
+        from .util import HostStream
+        if isinstance(Xd, HostStream):
+            rows = min(rows, Xd.chunk_rows)
         dims = [int(A.shape[0]) for A in self.Bcp[:-1]]
         if list(Xd.shape[1:]) != dims:
             raise ValueError(f"Incorrect shapes for inner product along {len(dims)} common modes. "
@@ -152,16 +164,63 @@ class CP_logistic_regression():
             self._plan = p
         return p
 
-    def _class_weights(self, weights, dev, yd, process_group=None):
+    def _sync_class_set(self, process_group):
+        """The class set of a sample-sharded fit is the union of every rank's labels.
+
+        The reference takes n_classes = len(unique(y)) from the data it is given
+        (multinomial_tensor_regression.py:279-280) and CrossEntropyLoss then requires every label
+        to be < n_classes.  A rank's shard may miss classes, so under a process group the count is
+        taken from all ranks' labels (MAX all-reduce of the label range, then of a presence
+        bitmap), and every rank raises the reference's own error when the union is not
+        0..C-1 — the same error a single process on the concatenated data would raise.  A class
+        factor this model drew from its local labels is widened to the global count (the new rows
+        drawn like make_BcpInit's); the fit then starts every rank from group rank 0's parameters
+        (sync_replicas).  A caller's Bcp_init keeps its shape, and must cover the labels."""
+        import torch.distributed as dist
+        cdev = _engine.collective_device(process_group)
+        y = torch.as_tensor(self.y).reshape(-1).to(cdev, torch.long)
+        n = y.numel()
+        rng = torch.tensor([int(y.max()) if n else -1, -int(y.min()) if n else 0, n], dtype=torch.int64, device=cdev)
+        nn_ = rng[2:].clone()
+        dist.all_reduce(rng, op=dist.ReduceOp.MAX, group=process_group)
+        dist.all_reduce(nn_, group=process_group)
+        ymax, ymin, n_all = int(rng[0]), -int(rng[1]), int(nn_[0])
+        if n_all == 0:
+            raise ValueError("the sharded multinomial fit got no samples on any rank")
+        if ymin < 0:
+            raise IndexError(f"Target {ymin} is out of bounds.")
+        if ymax >= n_all:  # fewer samples than label values: the union cannot be 0..ymax
+            raise IndexError(f"Target {ymax} is out of bounds.")
+        present = torch.zeros(ymax + 1, dtype=torch.int32, device=cdev)
+        if n:
+            present[y] = 1
+        dist.all_reduce(present, op=dist.ReduceOp.MAX, group=process_group)
+        C = int(present.sum())
+        if self._class_factor_auto:
+            if C != ymax + 1:  # reference: n_classes = C < ymax + 1 -> label ymax out of bounds
+                raise IndexError(f"Target {ymax} is out of bounds.")
+            A = self.Bcp[-1]
+            if int(A.shape[0]) != C:
+                extra = (torch.rand((C - int(A.shape[0]), self.rank)) * self._Bcp_init_scale
+                         - (1 - self.non_negative[-1]) * (self._Bcp_init_scale / 2)).to(A.device)
+                with torch.no_grad():
+                    self.Bcp[-1] = torch.cat([A.detach(), extra.to(A.dtype)], dim=0).requires_grad_(True)
+                self._plan = None
+                self._dev_cache = None
+            self.n_classes = C
+        Cm = int(self.Bcp[-1].shape[0])
+        _engine.check_uniform(Cm, process_group, "the number of classes (class-factor rows)", cdev)
+        if ymax >= Cm:
+            raise IndexError(f"Target {ymax} is out of bounds.")
+
+    def _class_weights(self, weights, dev, yd):
+        """The class weights on the device and this rank's CE normaliser sum_n w[y_n]."""
         cw = torch.as_tensor(weights, dtype=torch.float32).to(f"cuda:{dev}").contiguous()
         C = int(self.Bcp[-1].shape[0])
         if cw.ndim != 1 or cw.numel() != C:
             raise RuntimeError(f"weight tensor should be defined either for all {C} classes or no classes "
                                f"but got weight tensor of shape: {list(cw.shape)}")
         W = cw.double()[yd].sum()
-        if process_group is not None:
-            import torch.distributed as dist
-            dist.all_reduce(W, group=process_group)
         return cw, float(W.item())
 
     # ---- fitting -------------------------------------------------------------------------------
@@ -171,6 +230,8 @@ class CP_logistic_regression():
         if LBFGS_kwargs is None:
             raise TypeError("torch.optim.lbfgs.LBFGS() argument after ** must be a mapping, not NoneType")
         dev, Xd, yd = self._device_data()
+        if not isinstance(Xd, torch.Tensor):
+            raise NotImplementedError("the LBFGS fit needs X resident on the device (use fit_Adam for a HostStream)")
         plan = self._get_plan(Xd, Xd.shape[0])
         cw, W = self._class_weights(weights, dev, yd)
         optimizer = torch.optim.LBFGS(self.Bcp, **LBFGS_kwargs)
@@ -214,11 +275,23 @@ class CP_logistic_regression():
         process_group: optional torch.distributed group; self.X / self.y are then this rank's
         sample shard (the CE normaliser sum_n w[y_n] is all-reduced once)."""
         hp = adam_hparams(Adam_kwargs)
-        dev, Xd, yd = self._device_data()
-        plan = self._get_plan(Xd, Xd.shape[0])
-        if process_group is not None:
-            _engine.check_uniform(int(self.Bcp[-1].shape[0]), process_group, "the number of classes", Xd.device)
-        cw, W = self._class_weights(weights, dev, yd, process_group)
+
+        def prepare():
+            dev, Xd, yd = self._device_data()
+            plan = self._get_plan(Xd, Xd.shape[0])
+            cw, W = self._class_weights(weights, dev, yd)
+            return dev, Xd, yd, plan, cw, W
+        if process_group is None:
+            dev, Xd, yd, plan, cw, W = prepare()
+        else:
+            # collectives first, then the rank-local checks with a collective verdict: a failure on
+            # one rank raises on every rank instead of leaving the others in a later all-reduce
+            self._sync_class_set(process_group)
+            dev, Xd, yd, plan, cw, W = _engine.agree(process_group, prepare)
+            import torch.distributed as dist
+            Wt = torch.tensor([W], dtype=torch.float64, device=f"cuda:{dev}")
+            dist.all_reduce(Wt, group=process_group)
+            W = float(Wt.item())
         arena = plan.pack(self.Bcp)
         w = self.weights.to(f"cuda:{dev}", torch.float32).contiguous()
         vcb = _Verbose() if verbose == 2 else None
@@ -233,11 +306,17 @@ class CP_logistic_regression():
     def predict(self, X=None, y_true=None, Bcp=None, device=None):
         """(probabilities, argmax) as numpy (multinomial…py:474-545); the 'logit' the reference
         returns is the softmax output (quirk Q2)."""
+        from .util import HostStream
         if device is None:
             device = self.device
         if X is None:
             X = self.X
-        elif isinstance(X, torch.Tensor) is False:
+        if isinstance(X, HostStream):  # chunk by chunk through the same forward kernel
+            Bd = [torch.as_tensor(A).to(f"cuda:{X.dev_index}") for A in (self.Bcp if Bcp is None else Bcp)]
+            logit = torch.cat([model(Xc, Bd, self.weights, self.non_negative, softplus_kwargs=self.softplus_kwargs)
+                               for _, _, Xc in X.chunks()]).detach().cpu().numpy()
+            return logit, np.argmax(logit, axis=1)
+        if isinstance(X, torch.Tensor) is False:
             X = torch.tensor(X, dtype=torch.float32, requires_grad=False).to(device)
         elif X.device != torch.device(device):
             X = X.to(device)
@@ -278,7 +357,8 @@ class CP_logistic_regression():
 
     def get_params(self):
         # the reference reads a nonexistent self.bias here (quirk Q4); the working subset is returned
-        return {'X': self.X.detach().cpu().numpy(),
+        X = self.X.X if not isinstance(self.X, torch.Tensor) else self.X  # HostStream: its host tensor
+        return {'X': X.detach().cpu().numpy(),
                 'y': self.y.detach().cpu().numpy(),
                 'weights': self.weights.detach().cpu().numpy(),
                 'Bcp': self.detach_Bcp(),

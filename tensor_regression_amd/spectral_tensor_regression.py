@@ -368,8 +368,15 @@ class CP_linear_regression():
         and the per-iteration gradient arena is summed with one all-reduce.
         """
         hp = adam_hparams(Adam_kwargs)
-        X, y, dev = self._inputs(X, y)
-        plan = self._get_plan(X, X.shape[0])
+        from .util import HostStream
+
+        def prepare():
+            Xd, yd, dev = self._inputs(X, y)
+            if verbose in (2, 3) and isinstance(Xd, HostStream):
+                raise NotImplementedError("verbose=2/3 (per-iteration y_hat variance) is not offered for a HostStream X")
+            return Xd, yd, dev, self._get_plan(Xd, Xd.shape[0])
+        # under a process group a rank-local failure raises on every rank (_engine.agree)
+        X, y, dev, plan = prepare() if process_group is None else _engine.agree(process_group, prepare)
         n_global = float(X.shape[0])
         if process_group is not None:
             import torch.distributed as dist
@@ -379,9 +386,6 @@ class CP_linear_regression():
         norm = n_global * y.shape[1]
         arena = self._arena(plan)
         w = self._weights(dev)
-        from .util import HostStream
-        if verbose in (2, 3) and isinstance(X, HostStream):
-            raise NotImplementedError("verbose=2/3 (per-iteration y_hat variance) is not offered for a HostStream X")
         vcb = _VerbosePrinter(plan, X, y, w, norm) if verbose in (2, 3) else None
         convergence_reached, _ = run_adam_fit(plan, X, y, None, norm, arena, w, lambda_L2, max_iter, tol, patience,
                                               hp, self.loss_running, verbose_cb=vcb, process_group=process_group)

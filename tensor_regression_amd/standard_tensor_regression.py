@@ -284,12 +284,16 @@ class CP_linear_regression():
         shard and the per-iteration gradient arena is summed with one all-reduce.
         """
         hp = adam_hparams(Adam_kwargs)
-        X, y, dev = self._inputs(X, y)
-        plan = self._get_plan(X, X.shape[0])
-        n_global = float(X.shape[0])
         from .util import HostStream
-        if verbose == 2 and isinstance(X, HostStream):
-            raise NotImplementedError("verbose=2 (per-iteration y_hat variance) is not offered for a HostStream X")
+
+        def prepare():
+            Xd, yd, dev = self._inputs(X, y)
+            if verbose == 2 and isinstance(Xd, HostStream):
+                raise NotImplementedError("verbose=2 (per-iteration y_hat variance) is not offered for a HostStream X")
+            return Xd, yd, dev, self._get_plan(Xd, Xd.shape[0])
+        # under a process group a rank-local failure raises on every rank (_engine.agree)
+        X, y, dev, plan = prepare() if process_group is None else _engine.agree(process_group, prepare)
+        n_global = float(X.shape[0])
         if process_group is not None:
             import torch.distributed as dist
             n_t = torch.tensor([X.shape[0]], dtype=torch.float64, device=f"cuda:{dev}")

@@ -111,6 +111,14 @@ class HostStream:
     def __len__(self):
         return self.shape[0]
 
+    @property
+    def ndim(self):
+        return len(self.shape)
+
+    @property
+    def dtype(self):
+        return self.X.dtype
+
     def chunks(self):
         """Yield (r0, r1, device view) in order; copies run one chunk ahead on copy_stream."""
         N = self.shape[0]
@@ -125,8 +133,9 @@ class HostStream:
                 self.bufs[b][: r1 - r0].copy_(self.X[r0:r1], non_blocking=True)
                 self.copied[b].record(self.copy_stream)
 
-        for b in range(2):  # both buffers start free
-            self.consumed[b].record(compute)
+        # a buffer is free once the kernels of the last chunk that used it have run: the first
+        # copies of an iteration wait only for those (an event never recorded is complete), so
+        # they overlap the end of the previous iteration (its last chunks, reduction, Adam step)
         if bounds:
             issue(0)
         for c, (r0, r1) in enumerate(bounds):

@@ -154,14 +154,16 @@ def _worker(rank, world, port, model, tol, out_path, variant="plain"):
 
 
 def _worker_mismatch(rank, world, port, out_path):
-    """Rank 1's model has a different arena size (a multinomial shard missing a class): every rank
-    must raise instead of hanging in the per-iteration all-reduce."""
+    """Rank 1's model has other feature shapes (a genuine mismatch: a class count that differs
+    between shards is resolved before the fit, CP_logistic_regression._sync_class_set): every
+    rank must raise instead of hanging in the per-iteration all-reduce."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     X, y, cw, norm, shapes, arena0 = _problem("multinomial")
     if rank == 1:
-        shapes = shapes[:-1] + [(shapes[-1][0] - 1, shapes[-1][1])]
+        shapes = [(shapes[0][0] - 1, shapes[0][1])] + shapes[1:]
+        X = X[:, :-1]
         arena0 = arena0[:sum(a * b for a, b in shapes)]
     try:
         _fit("multinomial", X, y, cw, norm, shapes, arena0, process_group=dist.group.WORLD, iters=3)
@@ -234,3 +236,126 @@ def test_rank_mismatch_raises_everywhere(tmp_path):
     for r in range(2):
         with open(f"{out}.{r}") as f:
             assert f.read() == "ValueError"
+
+
+# ------------------------------------------------------------------------------------------------
+# host logic of the sharded multinomial fit: the global class set (multinomial…py:279-280 takes
+# n_classes = len(unique(y)) from the data it is given) and collective failure of local checks
+# ------------------------------------------------------------------------------------------------
+def _init(rank, world, port):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+
+
+def _labels(variant, rank):
+    """rank 0 / rank 1 label shards of a 10-class problem."""
+    g = torch.Generator().manual_seed(3 + rank)
+    y = torch.randint(0, 10, (60,), generator=g)
+    if variant == "missing_middle_top":  # rank 1 lacks classes 4 and 9
+        if rank == 0:
+            y[:10] = torch.arange(10)
+        else:
+            y[(y == 4) | (y == 9)] = 0
+    elif variant == "rank0_missing":  # rank 0 (whose parameters are broadcast) lacks class 9
+        if rank == 0:
+            y[y == 9] = 1
+        else:
+            y[:10] = torch.arange(10)
+    elif variant == "union_gap":  # class 5 on no rank: the reference's IndexError, on every rank
+        y[y == 5] = 6
+        y[:1] = 9
+    elif variant == "negative":
+        if rank == 1:
+            y[3] = -1
+    elif variant == "empty_rank":
+        y = y[:0] if rank == 1 else torch.cat([torch.arange(10), y])
+    return y
+
+
+def _worker_classes(rank, world, port, variant, out_path):
+    from tensor_regression_amd import CP_logistic_regression
+    _init(rank, world, port)
+    y = _labels(variant, rank)
+    X = torch.zeros(y.shape[0], 4, 3)
+    torch.manual_seed(11 + rank)
+    m = CP_logistic_regression(X, y, rank=2)
+    res = {"local_C": int(m.Bcp[-1].shape[0])}
+    try:
+        m._sync_class_set(dist.group.WORLD)
+        res.update(ok=True, C=int(m.Bcp[-1].shape[0]), n_classes=int(m.n_classes),
+                   head=m.Bcp[-1].detach()[:res["local_C"]].clone(), requires_grad=bool(m.Bcp[-1].requires_grad))
+    except IndexError as e:
+        res.update(ok=False, err=str(e))
+    torch.save(res, f"{out_path}.{rank}")
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("variant", ["missing_middle_top", "rank0_missing", "union_gap", "negative", "empty_rank"])
+def test_sharded_class_set(tmp_path, variant):
+    out = str(tmp_path / "cls")
+    mp.spawn(_worker_classes, args=(2, _free_port(), variant, out), nprocs=2, join=True)
+    r = [torch.load(f"{out}.{k}", weights_only=True) for k in range(2)]
+    if variant in ("union_gap", "negative"):
+        # the error a single process on the concatenated labels raises, on every rank
+        want = "Target 9 is out of bounds." if variant == "union_gap" else "Target -1 is out of bounds."
+        assert [x["ok"] for x in r] == [False, False] and [x["err"] for x in r] == [want, want]
+        return
+    assert all(x["ok"] for x in r)
+    assert [x["C"] for x in r] == [10, 10] and [x["n_classes"] for x in r] == [10, 10]
+    assert all(x["requires_grad"] for x in r)
+    # the locally drawn rows are kept; only the missing class rows are appended
+    assert all(x["head"].shape[0] == x["local_C"] for x in r)
+    if variant == "missing_middle_top":
+        assert [x["local_C"] for x in r] == [10, 8]
+    if variant == "empty_rank":
+        assert r[1]["local_C"] == 0
+
+
+def _worker_agree(rank, world, port, out_path):
+    """_engine.agree: a local check that fails on rank 1 only raises on both ranks (rank 1 its own
+    error, rank 0 a RuntimeError), and the group stays usable; then the production fit_Adam on a
+    host without a HIP device fails the same way on every rank instead of hanging."""
+    from tensor_regression_amd import CP_logistic_regression, CP_linear_regression, _engine
+    _init(rank, world, port)
+    res = []
+
+    def local():
+        if rank == 1:
+            raise ValueError("rank-1 only")
+        return 5
+    try:
+        res.append(("agree", _engine.agree(dist.group.WORLD, local)))
+    except Exception as e:
+        res.append(("agree", type(e).__name__))
+    t = torch.ones(1)
+    dist.all_reduce(t)
+    res.append(("after", float(t)))
+    y = _labels("missing_middle_top", rank)
+    m = CP_logistic_regression(torch.zeros(y.shape[0], 4, 3), y, rank=2)
+    try:
+        m.fit_Adam(max_iter=2, weights=np.ones(10), Adam_kwargs={"lr": 0.1}, process_group=dist.group.WORLD)
+        res.append(("mnl", "no error"))
+    except Exception as e:
+        res.append(("mnl", type(e).__name__))
+    lm = CP_linear_regression((8, 4, 3), rank=2)
+    try:
+        lm.fit_Adam(torch.zeros(8, 4, 3), torch.zeros(8), Adam_kwargs={"lr": 0.1}, process_group=dist.group.WORLD)
+        res.append(("lin", "no error"))
+    except Exception as e:
+        res.append(("lin", type(e).__name__))
+    with open(f"{out_path}.{rank}", "w") as f:
+        f.write(repr(res))
+    dist.destroy_process_group()
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-device failure path")
+def test_local_failure_raises_on_every_rank(tmp_path):
+    out = str(tmp_path / "agree")
+    mp.spawn(_worker_agree, args=(2, _free_port(), out), nprocs=2, join=True)
+    r = [eval(open(f"{out}.{k}").read()) for k in range(2)]
+    assert r[0][0] == ("agree", "RuntimeError") and r[1][0] == ("agree", "ValueError")
+    assert r[0][1] == r[1][1] == ("after", 2.0)
+    for k in range(2):
+        assert r[k][2] == ("mnl", "HipLibraryError") and r[k][3] == ("lin", "HipLibraryError"), r[k]

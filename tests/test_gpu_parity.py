@@ -150,10 +150,26 @@ def test_linear_golden(name, kind):
 @pytest.mark.parametrize("name", MNL)
 def test_multinomial_golden(name, kind):
     with path(kind):
-        _multinomial_golden(name)
+        _multinomial_golden(name, kind)
 
 
-def _multinomial_golden(name):
+def _assert_probs(got, ref32, X, Bcp, m):
+    """Forward probabilities: elementwise within rtol 1e-5 / atol 1e-6 of the reference, or no
+    further from the fp64 restatement than the reference's own fp32 output is (x2, + 1e-6).  The
+    second arm matters only for logits of large magnitude over long rows: mnl_duo_t has |Z| up to
+    58 over P = 8192 features, where the reference's own fp32 probabilities are 3e-6 from the
+    exact ones — its rounding noise, not a bar to match to 1e-6."""
+    from oracle import cp_oracle
+    ok = np.abs(got - ref32) <= RTOL * np.abs(ref32) + 1e-6
+    if not ok.all():
+        p64 = cp_oracle.mnl_model(X.double(), [torch.tensor(a).double() for a in Bcp],
+                                  torch.ones(m["rank"], dtype=torch.float64), m["non_negative"],
+                                  m["softplus_kwargs"]).numpy()
+        ok |= np.abs(got - p64) <= 2 * np.abs(ref32 - p64) + 1e-6
+    assert ok.all(), (np.abs(got - ref32).max(), got[~ok][:5], ref32[~ok][:5])
+
+
+def _multinomial_golden(name, kind="auto"):
     from tensor_regression_amd import CP_logistic_regression
     from tensor_regression_amd.multinomial_tensor_regression import model as mnl_model
     d = load(name)
@@ -162,9 +178,16 @@ def _multinomial_golden(name):
     mm = CP_logistic_regression(d["X"].numpy(), d["y"], rank=m["rank"], non_negative=m["non_negative"],
                                 Bcp_init=Bcp, device=DEV, softplus_kwargs=m["softplus_kwargs"])
     S = mnl_model(mm.X, mm.Bcp, mm.weights, mm.non_negative, mm.softplus_kwargs)
-    np.testing.assert_allclose(S.cpu().numpy(), d["probs0"], rtol=RTOL, atol=1e-6)
+    _assert_probs(S.cpu().numpy(), d["probs0"], d["X"], d["Bcp0_list"], m)
     dev, Xd, yd = mm._device_data()
     plan = mm._get_plan(Xd, Xd.shape[0])
+    if name.startswith("mnl_duo"):
+        # the fixtures at config 3's sample shapes pin the kernel config 3 runs (k_mnl_duo: its
+        # epilogue uses the hardware exp2/log2 units, so it is pinned separately from k_mnl_fused)
+        want = {"auto": " duo ", "noduo": "mnl-fused-1pass", "spi1": "mnl-fused-1pass"}.get(kind, "2pass")
+        assert want in plan.describe, plan.describe
+        if kind in ("noduo", "spi1"):
+            assert " duo " not in plan.describe, plan.describe
     cw, W = mm._class_weights(np.array(m["class_weights"]), dev, yd)
     arena = plan.pack(mm.Bcp)
     grad = torch.zeros(plan.num_grads, device=DEV)

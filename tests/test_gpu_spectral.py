@@ -93,13 +93,25 @@ def test_spectral_golden(name, kind):
         _spectral_golden(name, kind)
 
 
+@pytest.mark.parametrize("name", [n for n in SPEC if n.startswith("spec_slice")])
+def test_spectral_slice_golden_lockstep(name):
+    """the config-5-shaped fixtures through the whole-sample lock-step kernel as well"""
+    with spec_path("lockstep"):
+        _spectral_golden(name, "lockstep")
+
+
 def _spectral_golden(name, kind):
     d = load_spectral(name)
     m = d["meta"]
     X = d["X"].to(DEV)
     y = torch.tensor(d["y"], device=DEV)
     model = _model_from(d)
-    assert ("generic" in model._get_plan(X, X.shape[0]).describe) == (kind == "generic")
+    desc = model._get_plan(X, X.shape[0]).describe
+    assert ("generic" in desc) == (kind == "generic"), desc
+    if name.startswith("spec_slice"):
+        # fixtures at config 5's sample shape (W = 256, D = 129 / 100) pin the kernel config 5
+        # trains with (k_spec_slice) to the reference's own fit_Adam trajectory
+        assert ("slice-1pass" in desc) == (kind == "fused"), desc
     # predict() = lin_model + spectral_model (spectral…py:959-960)
     _close(model.predict(X).numpy(), d["predict0"])
     # one forward + loss + gradient (fit model, spectral…py:716-720)

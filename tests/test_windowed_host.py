@@ -231,14 +231,18 @@ def test_windowed_linear_golden(name, source):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("source", ["view", "materialised"])
+@pytest.mark.parametrize("source", ["view", "materialised", "hoststream"])
 def test_windowed_multinomial_golden(source):
     from tensor_regression_amd import CP_logistic_regression
     d = load("win_mnl")
     m = d["meta"]
     Xw, yw = _windows(d)
-    XX = (util.windowed_view(d["X"].to(DEV), torch.tensor(d["y_series"], device=DEV), m["win_range"])[0]
-          if source == "view" else Xw.contiguous().to(DEV))
+    if source == "view":
+        XX = util.windowed_view(d["X"].to(DEV), torch.tensor(d["y_series"], device=DEV), m["win_range"])[0]
+    elif source == "materialised":
+        XX = Xw.contiguous().to(DEV)
+    else:  # host-resident windows streamed through two device buffers, 3 chunks per iteration
+        XX = util.HostStream(Xw.contiguous(), chunk_rows=max(1, Xw.shape[0] // 3), device=DEV)
 
     def make():
         return CP_logistic_regression(XX, yw.numpy(), rank=m["rank"], device=DEV,
@@ -246,8 +250,11 @@ def test_windowed_multinomial_golden(source):
 
     from tensor_regression_amd.multinomial_tensor_regression import model as mnl_model
     mm = make()
-    S = mnl_model(XX, mm.Bcp, mm.weights, mm.non_negative, mm.softplus_kwargs)
-    np.testing.assert_allclose(S.cpu().numpy(), d["probs0"], rtol=1e-5, atol=1e-6)
+    if source == "hoststream":
+        S = mm.predict()[0]
+    else:
+        S = mnl_model(XX, mm.Bcp, mm.weights, mm.non_negative, mm.softplus_kwargs).cpu().numpy()
+    np.testing.assert_allclose(S, d["probs0"], rtol=1e-5, atol=1e-6)
     m10 = make()
     m10.fit_Adam(lambda_L2=m["lambda_L2"], max_iter=10, tol=0, patience=10, weights=np.ones(m["n_classes"]),
                  Adam_kwargs=m["adam_kwargs"])
@@ -256,3 +263,37 @@ def test_windowed_multinomial_golden(source):
     mm.fit_Adam(lambda_L2=m["lambda_L2"], max_iter=m["max_iter"], tol=0, patience=10,
                 weights=np.ones(m["n_classes"]), Adam_kwargs=m["adam_kwargs"])
     np.testing.assert_allclose(mm.loss_running, d["loss_running"], rtol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["spec_basic", "spec_nonneg_amsgrad_wd", "spec_slice_shape"])
+def test_spectral_hoststream_golden(name):
+    """The spectral fit_Adam (spectral…py:652-743) over a HostStream of the fixture's X (3 chunks
+    per iteration, each chunk's arena summed like a shard) against the reference's fixture: the
+    10-iteration loss trajectory and factors and the full trajectory at 1e-5, predict() at 1e-5."""
+    from golden_util import load_spectral
+    from tensor_regression_amd.spectral_tensor_regression import CP_linear_regression as SpecCP
+    d = load_spectral(name)
+    m = d["meta"]
+    X = d["X"]
+    y = torch.tensor(d["y"], device=DEV)
+    hs = util.HostStream(X.contiguous(), chunk_rows=max(1, X.shape[0] // 3), device=DEV)
+
+    def make():
+        Bn = [torch.tensor(a, device=DEV).requires_grad_(True) for a in d["Bcp_n0_list"]]
+        Bc = [torch.tensor(a, device=DEV).requires_grad_(True) for a in d["Bcp_c0_list"]]
+        return SpecCP(X.shape, (X.shape[0], m["n_out"]), rank_normal=m["rank_normal"],
+                      rank_spectral=m["rank_spectral"], non_negative=m["non_negative"], Bcp_init=(Bn, Bc),
+                      n_complex_dim=m["n_complex_dim"], device=DEV, softplus_kwargs=m["softplus_kwargs"])
+
+    m10 = make()
+    m10.fit_Adam(hs, y, lambda_L2=m["lambda_L2"], max_iter=min(10, m["max_iter"]), tol=m["tol"],
+                 patience=m["patience"], Adam_kwargs=m["adam_kwargs"])
+    np.testing.assert_allclose(m10.loss_running, d["loss_running_10"], rtol=1e-5)
+    _assert_close_factors(m10.Bcp_n, [a for a in d["Bcp_n_10_list"]])
+    _assert_close_factors(m10.Bcp_c, [a for a in d["Bcp_c_10_list"]])
+    model = make()
+    conv = model.fit_Adam(hs, y, lambda_L2=m["lambda_L2"], max_iter=m["max_iter"], tol=m["tol"],
+                          patience=m["patience"], Adam_kwargs=m["adam_kwargs"])
+    assert int(conv) == int(d["converged"]) and len(model.loss_running) == len(d["loss_running"])
+    np.testing.assert_allclose(model.loss_running, d["loss_running"], rtol=1e-5)

@@ -413,7 +413,8 @@ def kat_replay():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--kat", action="store_true")
-    ap.add_argument("--only", default=None, help="generate only the cases whose name starts with this prefix")
+    ap.add_argument("--only", default=None,
+                    help="generate only the cases whose name starts with one of these comma-separated prefixes")
     args = ap.parse_args()
     os.makedirs(OUT, exist_ok=True)
     torch.set_num_threads(1)  # fixed summation order for the golden outputs
@@ -422,7 +423,7 @@ def main():
         _save = save
 
         def save(name, **arrays):  # noqa: F811
-            if name.startswith(args.only):
+            if name.startswith(tuple(args.only.split(","))):
                 _save(name, **arrays)
     adam = {'lr': 0.01}
     linear_case("lin_basic", 11, (64, 8, 4), 2, [False, False, False], 0.3, 0.01, adam, 50)
@@ -463,11 +464,19 @@ def main():
     mnl_case("mnl_c10", 23, (256, 16, 8), 10, 4, [False, False, False], [1.0] * 10, 0.01, adam, 50)
     mnl_case("mnl_converge", 24, (96, 4, 4), 2, 2, [False, False, False], [1, 1], 0.01, {'lr': 0.001}, 300,
              tol=0.01, patience=5)
+    # the shapes of the two round-2 hot kernels (k_mnl_duo: (., 128, 64) / (., 64, 128) at rank 5-8;
+    # k_spec_slice: W = 256, 97 <= D <= 130) fitted by the reference's own fit_Adam
+    mnl_case("mnl_duo_shape", 42, (96, 128, 64), 10, 8, [False, False, False], [1.0] * 10, 0.01, adam, 40)
+    mnl_case("mnl_duo_t", 43, (80, 64, 128), 6, 7, [True, False, True], [0.5, 2.0, 1.0, 1.5, 0.8, 1.2], 0.02,
+             {'lr': 0.01, 'amsgrad': True}, 40)
     init_case("init_rng")
     spectral_case("spec_basic", 31, (64, 12, 9), 3, 2, 2, 1, False, 0.01, adam, 50)
     spectral_case("spec_nonneg_amsgrad_wd", 32, (80, 16, 17), 2, 3, 2, 2, [True, False, True], 0.02,
                   {'lr': 0.02, 'amsgrad': True, 'weight_decay': 0.01, 'betas': (0.8, 0.99), 'eps': 1e-6}, 50)
     spectral_case("spec_c5_shape", 33, (128, 32, 33), 2, 8, 8, 1, False, 0.01, adam, 40)
+    spectral_case("spec_slice_shape", 44, (40, 256, 129), 2, 8, 8, 1, False, 0.01, adam, 40)
+    spectral_case("spec_slice_d100", 45, (32, 256, 100), 3, 3, 5, 1, [True, False, True], 0.02,
+                  {'lr': 0.02, 'amsgrad': True}, 30)
     spectral_case("spec_rn0", 34, (48, 8, 5), 2, 0, 3, 1, False, 0.01, adam, 30)
     spectral_case("spec_rs0", 35, (48, 8, 5), 2, 3, 0, 1, False, 0.01, adam, 30)
     spectral_case("spec_cc1_softplus", 36, (40, 6, 7), 4, 2, 3, 0, [True, True, True], 0.01, adam, 30,
