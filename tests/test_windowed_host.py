@@ -227,7 +227,17 @@ def test_windowed_linear_golden(name, source):
                    Adam_kwargs=m["adam_kwargs"])
     assert len(model.loss_running) == len(d["loss_running"])
     np.testing.assert_allclose(model.loss_running, d["loss_running"], rtol=1e-5)
-    _assert_close_factors(model.Bcp, d["Bcp_final_list"], tol=1e-4)
+    # final factors: within 1e-5 of the reference, or no further from the fp64 restatement of
+    # the same trajectory than the reference's own fp32 run is (x2) -- the long-horizon bar of
+    # test_gpu_parity.py (Adam amplifies fp32 reduction-order noise)
+    from oracle import cp_oracle
+    r64 = cp_oracle.fit_adam_linear(Xw.contiguous(), yw, d["Bcp0_list"], d["bias0"], np.ones(m["rank"]),
+                                    m["non_negative"], m["lambda_L2"], m["max_iter"], 0.0, 10, m["adam_kwargs"],
+                                    m["softplus_kwargs"], dtype=torch.float64)
+    for a, b, c in zip(model.Bcp, d["Bcp_final_list"], r64["Bcp"]):
+        a = a.detach().cpu().numpy()
+        if normwise_rel(a, b) > 1e-5:
+            assert normwise_rel(a, c) <= 2 * normwise_rel(b, c) + 1e-5, (normwise_rel(a, b), normwise_rel(a, c))
 
 
 @pytest.mark.gpu
