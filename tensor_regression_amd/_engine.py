@@ -173,7 +173,7 @@ class Plan:
         self.describe = self.lib.tr_plan_describe(h).decode()
 
     def destroy(self):
-        """Release the C plan (idempotent).  tr_plan_destroy synchronises the plan's device first."""
+        """Release the C plan (idempotent); its hipFree orders the release after the work that uses it."""
         h = getattr(self, "h", None)
         if h is not None and h.value:
             self.h = None

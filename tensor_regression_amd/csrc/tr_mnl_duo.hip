@@ -16,8 +16,14 @@
 // Per sample k of a workgroup: wait own LDS-DMA of k -> barrier -> epilogue of k-1 (Z partials
 // of the 2 A-waves, double softmax, Wv, gradient scaling) -> GEMM of k with the DMA of k+1 into
 // the other ring slot interleaved.  The A-waves read Phi1 (their B operand) from a transposed
-// LDS table instead of 128 resident registers.  Numerics: the unit arithmetic, the Z partial
-// slots, the summation orders and the slab accumulation order are those of k_mnl_fused.
+// LDS table instead of 128 resident registers.  Numerics: the GEMM units, the Z partial slots and
+// the slab accumulation order are those of k_mnl_fused, but the epilogue is NOT bitwise equal to
+// it: exp / log run on the hardware base-2 units (v_exp_f32 / v_log_f32 with a premultiplied
+// log2 e, ~1 ulp), the second softmax skips its max shift (S in [0, 1]), and Wv / <dS, S> are
+// re-associated into closed forms over independent class sums (below); the file is also built
+// with -fno-honor-nans.  It is pinned to the reference separately from k_mnl_fused, at the same
+// 1e-5 bars (test_multinomial_golden kinds auto / noduo, including the mnl_duo_* fixtures at
+// its own shapes).
 #include <cstdlib>
 #include <cstring>
 #include <type_traits>
