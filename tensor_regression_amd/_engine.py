@@ -129,6 +129,36 @@ def stream_handle(dev):
     return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
 
 
+def _pack_arena(srcs, n, dtype, device):
+    """Concatenate the flattened factors (and bias) into a fresh arena: one launch when they all
+    live on the plan's device in its dtype, else one copy per tensor."""
+    arena = torch.empty(n, dtype=dtype, device=device)
+    with torch.no_grad():
+        if sum(s.numel() for s in srcs) == n and all(s.device == arena.device and s.dtype == dtype for s in srcs):
+            torch.cat(srcs, out=arena)
+        else:
+            o = 0
+            for s in srcs:
+                arena[o:o + s.numel()].copy_(s)
+                o += s.numel()
+            if o != n:
+                raise ValueError(f"the parameters hold {o} values, the plan's arena {n}")
+    return arena
+
+
+def _unpack_arena(arena, offsets, dsts):
+    """Copy the arena's segments back into the caller's tensors in place (like an optimizer step):
+    one multi-tensor launch when they all live on the arena's device in its dtype."""
+    bounds = list(offsets[:len(dsts)]) + [arena.numel()]
+    with torch.no_grad():
+        srcs = [arena[bounds[i]:bounds[i + 1]][:d.numel()].view(d.shape) for i, d in enumerate(dsts)]
+        if all(d.device == arena.device and d.dtype == arena.dtype for d in dsts):
+            torch._foreach_copy_(dsts, srcs)
+        else:
+            for d, s in zip(dsts, srcs):
+                d.copy_(s.to(device=d.device, dtype=d.dtype))
+
+
 class Plan:
     """Owns one `tr_plan` (workspace + kernel strategy) for a model shape."""
 
@@ -196,28 +226,23 @@ class Plan:
         return [(d, self.rank) for d in dims]
 
     def pack(self, Bcp, bias=None):
-        arena = torch.empty(self.num_params, dtype=self.dtype, device=f"cuda:{self.dev}")
         shapes = self.factor_shapes()
         if len(Bcp) != len(shapes):
             raise ValueError(f"expected {len(shapes)} Kruskal factors, got {len(Bcp)}")
-        with torch.no_grad():
-            for f, (A, shp) in enumerate(zip(Bcp, shapes)):
-                A = torch.as_tensor(A)
-                if tuple(A.shape) != shp:
-                    raise ValueError(f"factor {f} has shape {tuple(A.shape)}, expected {shp}")
-                arena[self.offsets[f]:self.offsets[f + 1]].copy_(A.detach().reshape(-1))
-            if self.model == _lib.TR_MODEL_LINEAR:
-                arena[self.offsets[-1]:].copy_(torch.as_tensor(bias).detach().reshape(-1)[:1])
-        return arena
+        srcs = []
+        for f, (A, shp) in enumerate(zip(Bcp, shapes)):
+            A = torch.as_tensor(A)
+            if tuple(A.shape) != shp:
+                raise ValueError(f"factor {f} has shape {tuple(A.shape)}, expected {shp}")
+            srcs.append(A.detach().reshape(-1))
+        if self.model == _lib.TR_MODEL_LINEAR:
+            srcs.append(torch.as_tensor(bias).detach().reshape(-1)[:1])
+        return _pack_arena(srcs, self.num_params, self.dtype, self.device_str)
 
     def unpack_into(self, arena, Bcp, bias=None):
         """Write the arena back into the caller's tensors in place (like an optimizer step)."""
-        with torch.no_grad():
-            for f, A in enumerate(Bcp):
-                src = arena[self.offsets[f]:self.offsets[f + 1]].view(A.shape)
-                A.copy_(src.to(device=A.device, dtype=A.dtype))
-            if bias is not None and self.model == _lib.TR_MODEL_LINEAR:
-                bias.copy_(arena[self.offsets[-1]:].to(device=bias.device, dtype=bias.dtype).view(bias.shape))
+        dsts = list(Bcp) + ([bias] if bias is not None and self.model == _lib.TR_MODEL_LINEAR else [])
+        _unpack_arena(arena, self.offsets, dsts)
 
     def factor_views(self, arena):
         return [arena[self.offsets[f]:self.offsets[f + 1]].view(shp)
@@ -245,7 +270,10 @@ class Plan:
 
     def check_status(self):
         """Raise if a kernel of this plan reported a device-side failure (tr_plan_status: a wide-row
-        cluster exchange that timed out because the GPU was shared).  Synchronises the device."""
+        cluster exchange that timed out because the GPU was shared).  Only a plan whose pass can
+        fail on the device (may_fail_on_device) has anything to check; it synchronises the device."""
+        if not self.may_fail_on_device:
+            return
         torch.cuda.synchronize(self.dev)
         st = ctypes.c_int32(0)
         check(self.lib.tr_plan_status(self.h, ctypes.byref(st)), "tr_plan_status")
@@ -364,26 +392,21 @@ class SpectralPlan(Plan):
         return [(W, Rn, 1), (D, Rn, 1), (O, Rn, 1), (W, Rs, Cc), (D, Rs, 1), (O, Rs, 1)]
 
     def pack(self, Bcp_n, Bcp_c, bias):
-        arena = torch.empty(self.num_params, dtype=torch.float32, device=self.device_str)
         shapes = self.factor_shapes()
         facs = list(Bcp_n) + list(Bcp_c)
         if len(facs) != 6:
             raise ValueError(f"expected 3 + 3 Kruskal factors, got {len(Bcp_n)} + {len(Bcp_c)}")
-        with torch.no_grad():
-            for f, (A, shp) in enumerate(zip(facs, shapes)):
-                A = torch.as_tensor(A)
-                if tuple(A.shape) != shp:
-                    raise ValueError(f"factor {f} has shape {tuple(A.shape)}, expected {shp}")
-                arena[self.offsets[f]:self.offsets[f + 1]].copy_(A.detach().reshape(-1))
-            arena[self.offsets[6]:].copy_(torch.as_tensor(bias).detach().reshape(-1))
-        return arena
+        srcs = []
+        for f, (A, shp) in enumerate(zip(facs, shapes)):
+            A = torch.as_tensor(A)
+            if tuple(A.shape) != shp:
+                raise ValueError(f"factor {f} has shape {tuple(A.shape)}, expected {shp}")
+            srcs.append(A.detach().reshape(-1))
+        srcs.append(torch.as_tensor(bias).detach().reshape(-1))
+        return _pack_arena(srcs, self.num_params, torch.float32, self.device_str)
 
     def unpack_into(self, arena, Bcp_n, Bcp_c, bias=None):
-        with torch.no_grad():
-            for f, A in enumerate(list(Bcp_n) + list(Bcp_c)):
-                A.copy_(arena[self.offsets[f]:self.offsets[f + 1]].view(A.shape).to(device=A.device, dtype=A.dtype))
-            if bias is not None:
-                bias.copy_(arena[self.offsets[6]:].to(device=bias.device, dtype=bias.dtype).view(bias.shape))
+        _unpack_arena(arena, self.offsets, list(Bcp_n) + list(Bcp_c) + ([bias] if bias is not None else []))
 
     def forward(self, X, arena, weights, out=None):
         """The reference's predict model: lin_model + spectral_model (N, n_out)."""
@@ -512,6 +535,26 @@ def sync_replicas(arena, process_group):
     dist.broadcast(arena, src=src, group=process_group)
 
 
+def fit_state(plan, dtype, amsgrad):
+    """(grad, m, v, vmax | None, stop, tmp) of one Adam fit: views of ONE per-plan device buffer,
+    zeroed with a single fill per fit (one launch instead of six allocations and fills).  The
+    buffer is reused by the plan's next fit; fits on one plan run one after another, and each
+    ends in a host synchronisation on its final status before it returns."""
+    G, P = plan.num_grads, plan.num_params
+    seg = lambda n: -(-n // 64) * 64  # 256-byte aligned segments
+    sizes = (seg(G), seg(P), seg(P), seg(P), seg(G), 64)
+    n = sum(sizes)
+    buf = getattr(plan, "_fit_state", None)
+    if buf is None or buf.numel() != n or buf.dtype != dtype:
+        buf = torch.empty(n, dtype=dtype, device=plan.device_str)
+        plan._fit_state = buf
+    buf.zero_()
+    parts = torch.split(buf, sizes)
+    grad, m, v, vmax, tmp = parts[0][:G], parts[1][:P], parts[2][:P], parts[3][:P], parts[4][:G]
+    stop = parts[5].view(torch.int32)[:1]
+    return grad, m, v, (vmax if amsgrad else None), stop, tmp
+
+
 def run_adam_fit(plan, X, target, class_weight, norm, arena, weights, lambda_L2, max_iter, tol, patience,
                  hp, loss_running, verbose_cb=None, process_group=None, sync_every=64):
     """The fit_Adam loop (standard…py:453-470 / multinomial…py:447-465), device resident.
@@ -531,17 +574,13 @@ def run_adam_fit(plan, X, target, class_weight, norm, arena, weights, lambda_L2,
 
         def allreduce(g):
             dist.all_reduce(g, group=process_group)
-    opts = dict(dtype=fdt, device=dev)
-    grad = torch.zeros(plan.num_grads, **opts)
-    m = torch.zeros(plan.num_params, **opts)
-    v = torch.zeros(plan.num_params, **opts)
-    vmax = torch.zeros(plan.num_params, **opts) if hp["amsgrad"] else None
+    grad, m, v, vmax, stop, tmp = fit_state(plan, fdt, hp["amsgrad"])
     base = len(loss_running)
-    hist = torch.zeros(base + max(int(max_iter), 0) + 1, dtype=torch.float64, device=dev)
-    if base:
+    # every entry a reader touches is written first: the loop writes [base, base + n_run) and the
+    # plateau test (launched only when tol > 0) also reads the earlier losses, which are copied in
+    hist = torch.empty(base + max(int(max_iter), 0) + 1, dtype=torch.float64, device=dev)
+    if base and tol > 0:
         hist[:base] = torch.tensor(loss_running, dtype=torch.float64)
-    stop = torch.zeros(1, dtype=torch.int32, device=dev)
-    tmp = torch.zeros_like(grad)
     if verbose_cb is not None:
         sync_every = 1
     # the loop changes the arena only through adam_step: let each step prepare the next

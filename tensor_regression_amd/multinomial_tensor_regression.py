@@ -207,6 +207,7 @@ class CP_logistic_regression():
                     self.Bcp[-1] = torch.cat([A.detach(), extra.to(A.dtype)], dim=0).requires_grad_(True)
                 self._plan = None
                 self._dev_cache = None
+                self._cw_cache = None
             self.n_classes = C
         Cm = int(self.Bcp[-1].shape[0])
         _engine.check_uniform(Cm, process_group, "the number of classes (class-factor rows)", cdev)
@@ -214,14 +215,22 @@ class CP_logistic_regression():
             raise IndexError(f"Target {ymax} is out of bounds.")
 
     def _class_weights(self, weights, dev, yd):
-        """The class weights on the device and this rank's CE normaliser sum_n w[y_n]."""
-        cw = torch.as_tensor(weights, dtype=torch.float32).to(f"cuda:{dev}").contiguous()
+        """The class weights on the device and this rank's CE normaliser sum_n w[y_n].  Both are
+        kept for the next fit on the same labels and weights (the normaliser costs a reduction
+        over the labels and a host synchronisation)."""
+        cwh = torch.as_tensor(weights, dtype=torch.float32).detach().cpu()
         C = int(self.Bcp[-1].shape[0])
-        if cw.ndim != 1 or cw.numel() != C:
+        if cwh.ndim != 1 or cwh.numel() != C:
             raise RuntimeError(f"weight tensor should be defined either for all {C} classes or no classes "
-                               f"but got weight tensor of shape: {list(cw.shape)}")
-        W = cw.double()[yd].sum()
-        return cw, float(W.item())
+                               f"but got weight tensor of shape: {list(cwh.shape)}")
+        key = (yd, yd._version, dev, cwh.numpy().tobytes())
+        c = getattr(self, "_cw_cache", None)
+        if c is not None and c[0] is key[0] and c[1:4] == key[1:]:
+            return c[4], c[5]
+        cw = cwh.to(f"cuda:{dev}").contiguous()
+        W = float(cw.double()[yd].sum().item())
+        self._cw_cache = key + (cw, W)
+        return cw, W
 
     # ---- fitting -------------------------------------------------------------------------------
     def fit(self, lambda_L2=0.01, max_iter=1000, tol=1e-5, patience=10, weights=None, verbose=False,
@@ -382,6 +391,7 @@ class CP_logistic_regression():
         self.loss_running = params['loss_running']
         self._plan = None
         self._dev_cache = None
+        self._cw_cache = None
 
     def display_params(self):
         print('X:', self.X.shape)

@@ -65,14 +65,20 @@ def main():
     a = res[50] - 50 * b
     print(f"{args.config}: per-iteration {1e3 * b:.4f} ms, per-call {1e3 * a:.3f} ms", flush=True)
     if args.profile:
+        reps = 50
         pr = cProfile.Profile()
         torch.cuda.synchronize()
         pr.enable()
-        fit(1)
+        for _ in range(reps):
+            fit(1)
         torch.cuda.synchronize()
         pr.disable()
-        pstats.Stats(pr).sort_stats("tottime").print_stats(25)
-
+        st = pstats.Stats(pr).stats
+        rows = sorted(((ct / reps, tt / reps, nc / reps, f"{os.path.basename(k[0])}:{k[1]}({k[2]})")
+                       for k, (cc, nc, tt, ct, _) in st.items()), reverse=True)
+        print(f"host profile of fit_Adam(max_iter=1), mean over {reps} calls (us): cum / own / calls per fit")
+        for ct, tt, nc, name in rows[:40]:
+            print(f"  {1e6 * ct:9.1f} {1e6 * tt:9.1f} {nc:6.1f}  {name}")
 
 if __name__ == "__main__":
     main()
