@@ -260,6 +260,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=None, help="CPU baseline threads (default: affinity size)")
     ap.add_argument("--time-all-kernels", action="store_true",
                     help="hipEvent-time every kernel kind (adds per-launch event overhead)")
+    ap.add_argument("--timing-every", type=int, default=1,
+                    help="bracket only every n-th launch of the timed kernels with HIP events (default: every launch)")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="no hipEvents in the timed region (ms_per_step without event packets; no roofline)")
     ap.add_argument("--traffic", default=os.path.join(HERE, "profiles", "traffic.json"),
@@ -326,10 +328,12 @@ def main():
         raise SystemExit(f"bench {args.config}: plan took an unexpected path ({plan.describe}); expected "
                          f"path={want} (--allow-other-path to measure it anyway)")
     plan.read_timing()
-    # time only the X-streaming kernels by default (2 events per stream launch): timing every
-    # tail launch adds event packets between kernels and inflates ms_per_step
+    # time only the X-streaming kernels by default (timing-only events, no system-scope fence:
+    # with the default fence each record idled the GPU ~6 us on its side of the launch in a
+    # rocprofv3 kernel trace; --timing-every n brackets only every n-th launch)
     if not args.no_kernel_timing:
-        plan.set_timing(True, kinds=None if args.time_all_kernels else ["stream_fused", "stream_rows", "stream_cols"])
+        plan.set_timing(True, kinds=None if args.time_all_kernels else ["stream_fused", "stream_rows", "stream_cols"],
+                        every=max(1, args.timing_every))
 
     def barrier():
         if pg is not None:
@@ -436,6 +440,8 @@ def main():
                      "kernel_avg_ms": dom_ms, "algorithmic_bytes_per_launch": bytes_launch},
         "kernel_avg_ms": kernel_avg,
     }
+    # the launches the kernel average is over (every --timing-every-th launch of the timed region)
+    out["roofline"].update({"timed_launches": int(kt[dom][1]), "timing_every": max(1, args.timing_every)})
     if hoststream is not None:
         out["hoststream"] = hoststream
         out["data"] += "; X resident in pinned host memory, copied to HBM every step (inside the timed region)"

@@ -270,7 +270,10 @@ int tr_spectral_latents(tr_plan* plan, const float* X, int64_t n_rows, const flo
  * `enable` is a bit mask over TR_KERNEL_* kinds (1 << kind; -1 = all): every launch of a
  * selected kind is bracketed by hipEvents on the caller's stream (no host synchronisation).  tr_plan_read_timing synchronises the recorded events and returns,
  * per kernel kind (TR_KERNEL_*), the summed elapsed milliseconds and the number of launches,
- * then clears the record.
+ * then clears the record.  tr_plan_set_timing_every(plan, n) brackets only the n-th, 2n-th, ...
+ * launch of each selected kind (n >= 1, default 1; tr_plan_set_timing restarts the count), for
+ * runs that must disturb the stream even less.  The events are timing-only (no system-scope
+ * fence when recorded).
  */
 #define TR_KERNEL_STREAM_FUSED 0 /* single-pass X stream (linear) */
 #define TR_KERNEL_STREAM_ROWS 1  /* two-pass forward X stream */
@@ -281,6 +284,7 @@ int tr_spectral_latents(tr_plan* plan, const float* X, int64_t n_rows, const flo
 #define TR_KERNEL_UPDATE 6       /* L2 + Adam + plateau test */
 #define TR_KERNEL_NKINDS 7
 int tr_plan_set_timing(tr_plan* plan, int enable);
+int tr_plan_set_timing_every(tr_plan* plan, int every);
 int tr_plan_read_timing(tr_plan* plan, double* total_ms /* [TR_KERNEL_NKINDS] */,
                         int64_t* launches /* [TR_KERNEL_NKINDS] */);
 

@@ -253,11 +253,13 @@ class Plan:
         """tr_plan_set_prepare_next: each adam_step also prepares the next loss_grad's factors."""
         check(self.lib.tr_plan_set_prepare_next(self.h, 1 if enable else 0), "tr_plan_set_prepare_next")
 
-    def set_timing(self, enable, kinds=None):
-        """Enable hipEvent timing for the given kernel kinds (names of _lib.KERNEL_KINDS; None = all)."""
+    def set_timing(self, enable, kinds=None, every=1):
+        """Enable hipEvent timing for the given kernel kinds (names of _lib.KERNEL_KINDS; None = all),
+        bracketing every `every`-th launch of each (tr_plan_set_timing_every)."""
         mask = 0
         if enable:
             mask = -1 if kinds is None else sum(1 << _lib.KERNEL_KINDS.index(k) for k in kinds)
+        check(self.lib.tr_plan_set_timing_every(self.h, int(every)), "tr_plan_set_timing_every")
         check(self.lib.tr_plan_set_timing(self.h, mask), "tr_plan_set_timing")
 
     def read_timing(self):

@@ -42,6 +42,7 @@ SIGNATURES = {
     "tr_loss_grad": (_c.c_int, [_vp, _vp, _c.c_int64, _vp, _vp, _c.c_double, _vp, _vp, _vp, _vp, _vp, _vp]),
     "tr_finalize_grad": (_c.c_int, [_vp, _vp, _vp, _c.c_float, _vp, _vp, _vp]),
     "tr_plan_set_timing": (_c.c_int, [_vp, _c.c_int]),
+    "tr_plan_set_timing_every": (_c.c_int, [_vp, _c.c_int]),
     "tr_plan_read_timing": (_c.c_int, [_vp, _c.POINTER(_c.c_double), _c.POINTER(_c.c_int64)]),
     "tr_plan_create_spectral": (_c.c_int, [_c.POINTER(_vp), _c.c_int, _c.c_int64, _c.c_int64, _c.c_int64, _c.c_int,
                                            _c.c_int, _c.c_int, _c.c_int64, _c.POINTER(_c.c_int32), _c.c_float,

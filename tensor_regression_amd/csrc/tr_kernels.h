@@ -112,5 +112,9 @@ hipError_t launch_converge(const double* loss_hist, int64_t hist_base, int64_t i
                            int32_t* stop, hipStream_t st);
 // whether k_update can prepare the next iteration in this mode for this factor set
 bool update_prepare_mode_ok(const FactorSet& fs, int mode);
+// MTTKRP of a two-factor model, one wave per factor row (tr_update.hip); launch_mttkrp uses it
+bool mttkrp2_supported(const FactorSet& fs);
+hipError_t launch_mttkrp2(const FactorSet& fs, const float* phi, const float* dphi, const float* w, const float* G,
+                          float* grad, const int32_t* stop, hipStream_t st);
 
 }  // namespace tr

@@ -10,8 +10,7 @@
 //       otherwise           -> k_rows + k_cols   two passes (forward rows, column reduction)
 //   (partials)            -> k_reduce_slabs       fixed-order slab sum (deterministic, no atomics)
 //   cp_to_tensor backward -> k_mttkrp             dPhi_f = G_(f) . KR(others) * w, chained through softplus'
-//   L2_penalty + Adam     -> k_update             norms, L2 grad, torch.optim.Adam/AMSGrad, loss record,
-//                                                 plateau test (device-side early stop)
+//   L2_penalty + Adam     -> k_update             (tr_update.hip)
 //
 // Every reduction is a fixed-order tree (wave butterfly, then LDS in wave order, then slabs
 // in index order) so a run is bitwise reproducible; no float atomics anywhere.
@@ -1033,188 +1032,6 @@ __global__ __launch_bounds__(256) void k_mttkrp(FactorSet fs, const float* __res
   }
 }
 
-// ==========================================================================================
-// K6: L2 term + Adam/AMSGrad + loss record + plateau test, single workgroup.
-//   L2_penalty (standard…py:180-196): sum_k sqrt(sum(A_k^2)) over RAW factors (not squared)
-//   d/dA [lambda*sqrt(sum A^2)] = (lambda / (2 ||A||)) * (2 A)     (Sqrt/Pow backward)
-//   torch/optim/adam.py _single_tensor_adam (torch 2.10), non-capturable branch.
-// numpy's pairwise summation is restated for np.sum(np.abs(np.diff(...))).
-// ==========================================================================================
-__device__ double np_pairwise_sum_absdiff(const double* h, int64_t n) {
-  // sum_{j<n} |h[j+1] - h[j]| in numpy's pairwise order (PW_BLOCKSIZE 128, 8 accumulators),
-  // iterative over the recursion tree (left-first), n <= 2^20.
-  double total = 0.0;
-  // explicit stack of (start, len, depth-combine) — emulate recursion with partial sums
-  struct Frame { int64_t s, n; int state; double left; };
-  Frame st[48];
-  int sp = 0;
-  st[sp++] = {0, n, 0, 0.0};
-  double ret = 0.0;
-  while (sp > 0) {
-    Frame& fr = st[sp - 1];
-    if (fr.n <= 128 && fr.state == 0) {
-      const int64_t s = fr.s, m = fr.n;
-      double res;
-      if (m < 8) {
-        res = -0.0;
-        for (int64_t i = 0; i < m; ++i) res += fabs(h[s + i + 1] - h[s + i]);
-      } else {
-        double r[8];
-        for (int j = 0; j < 8; ++j) r[j] = fabs(h[s + j + 1] - h[s + j]);
-        int64_t i = 8;
-        for (; i < m - (m % 8); i += 8)
-          for (int j = 0; j < 8; ++j) r[j] += fabs(h[s + i + j + 1] - h[s + i + j]);
-        res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-        for (; i < m; ++i) res += fabs(h[s + i + 1] - h[s + i]);
-      }
-      ret = res;
-      --sp;
-      continue;
-    }
-    int64_t n2 = fr.n / 2;
-    n2 -= n2 % 8;
-    if (fr.state == 0) {
-      fr.state = 1;
-      st[sp++] = {fr.s, n2, 0, 0.0};
-    } else if (fr.state == 1) {
-      fr.left = ret;
-      fr.state = 2;
-      const int64_t s = fr.s + n2, m = fr.n - n2;
-      st[sp++] = {s, m, 0, 0.0};
-    } else {
-      ret = fr.left + ret;
-      --sp;
-    }
-  }
-  total = ret;
-  return total;
-}
-
-// Next iteration's factor preparation from the just-updated factors (tr_plan_set_prepare_next):
-// softplus and its derivative, k_prep_factors' arithmetic, from the new values in LDS.
-__device__ void update_prepare_next(const FactorSet& fs, const PrepArgs& pa, const float* snew) {
-  __syncthreads();
-  for (int64_t k = threadIdx.x; k < fs.nfelem; k += blockDim.x) {
-    const float a = snew[k];
-    if (fs.nonneg[tr_factor_of(fs, k)]) {
-      pa.phi[k] = tr_softplus(a, pa.beta, pa.thr);
-      pa.dphi[k] = tr_softplus_grad(a, pa.beta, pa.thr);
-    } else {
-      pa.phi[k] = a;
-      pa.dphi[k] = 1.0f;
-    }
-  }
-}
-
-__global__ __launch_bounds__(1024) void k_update(FactorSet fs, int n_bias, float* __restrict__ params,
-                                                 const float* __restrict__ grad, UpdateArgs ua,
-                                                 float* __restrict__ m, float* __restrict__ v,
-                                                 float* __restrict__ vmax,
-                                                 float* __restrict__ grad_total_out,
-                                                 float* __restrict__ loss_out,
-                                                 double* __restrict__ loss_hist,
-                                                 int32_t* __restrict__ stop, PrepArgs pa) {
-#pragma clang fp contract(off)
-  extern __shared__ __attribute__((aligned(16))) float snew[];  // pa.mode > 0: the new factors
-  __shared__ float wsum[TR_MAXF * 16];
-  __shared__ float norms[TR_MAXF];
-  if (stop != nullptr && *stop != 0) return;
-  const int t = threadIdx.x;
-  const int lane = t & (TR_WAVE - 1);
-  const int q = t / TR_WAVE;
-  const int NWV = blockDim.x / TR_WAVE;
-  // a failed pass (status slot set, summed over shards by the all-reduce): stop the fit before
-  // the step so the parameters and the Adam state stay those of the last good iteration
-  if (ua.mode == 0 && stop != nullptr && grad[fs.nfelem + n_bias + 1] != 0.0f) {
-    if (t == 0) *stop = TR_STOP_DEVICE_ERROR - (int32_t)ua.iter;
-    return;
-  }
-  // ||A_f||_F of every factor (raw parameters) in one pass; fixed-order block reduction
-  {
-    float accn[TR_MAXF];
-#pragma unroll
-    for (int f = 0; f < TR_MAXF; ++f) accn[f] = 0.f;
-    for (int64_t k = t; k < fs.nfelem; k += blockDim.x) {
-      const float a = params[k];
-      const int f = tr_factor_of(fs, k);
-#pragma unroll
-      for (int g = 0; g < TR_MAXF; ++g)
-        if (g == f) accn[g] = fmaf(a, a, accn[g]);
-    }
-#pragma unroll
-    for (int f = 0; f < TR_MAXF; ++f) {
-      if (f < fs.nf) {
-        const float v = tr_wave_allreduce(accn[f]);
-        if (lane == 0) wsum[f * 16 + q] = v;
-      }
-    }
-    __syncthreads();
-    if (t < fs.nf) {
-      float tot = 0.f;
-      for (int k = 0; k < NWV; ++k) tot += wsum[t * 16 + k];
-      norms[t] = sqrtf(tot);
-    }
-    __syncthreads();
-  }
-  const int64_t nfe = fs.nfelem;
-  const int64_t np = nfe + n_bias;  // bias entries after the factors (linear 1, spectral n_out)
-  const float lam = ua.lambda_l2;
-  for (int64_t e = t; e < np; e += blockDim.x) {
-    float g = grad[e];
-    float p = params[e];
-    if (e < nfe) {
-      const int f = tr_factor_of(fs, e);
-      const float tt = lam / (2.0f * norms[f]);
-      g = g + tt * (2.0f * p);
-    }
-    if (ua.mode == 1) {
-      grad_total_out[e] = g;
-      continue;
-    }
-    if (ua.weight_decay != 0.0f) g = fmaf(p, ua.weight_decay, g);  // grad.add(param, alpha=wd)
-    float mm = m[e];
-    mm = fmaf(ua.one_minus_b1, g - mm, mm);                       // exp_avg.lerp_(grad, 1 - b1)
-    float vv = v[e] * ua.beta2;                                    // exp_avg_sq.mul_(b2)
-    vv = vv + ua.one_minus_b2 * g * g;                             //   .addcmul_(g, g, 1 - b2)
-    float den_src = vv;
-    if (ua.amsgrad) {
-      const float vm = fmaxf(vmax[e], vv);
-      vmax[e] = vm;
-      den_src = vm;
-    }
-    const float denom = sqrtf(den_src) / ua.bc2_sqrt + ua.eps;
-    p = p + (-ua.step_size) * (mm / denom);                        // addcdiv_(m, denom, -step_size)
-    m[e] = mm;
-    v[e] = vv;
-    params[e] = p;
-    if (pa.mode > 0 && e < nfe) snew[e] = p;
-  }
-  if (t == 0) {
-    float l2 = 0.f;
-    for (int f = 0; f < fs.nf; ++f) l2 = l2 + norms[f];
-    const float total = grad[np] + lam * l2;
-    if (loss_out != nullptr) *loss_out = total;
-    if (ua.mode == 0 && loss_hist != nullptr) loss_hist[ua.hist_base + ua.iter] = (double)total;
-    // spectral…py:738-741: `elif np.isnan(loss_running[-1])` only while ii <= patience;
-    // a negative flag = stopped without convergence, |flag| iterations run
-    if (ua.mode == 0 && ua.nan_stop && stop != nullptr && ua.iter <= ua.patience && __builtin_isnan(total))
-      *stop = -(int32_t)(ua.iter + 1);
-  }
-  if (ua.mode == 0 && pa.mode > 0) update_prepare_next(fs, pa, snew);
-}
-
-
-// Plateau test of fit_Adam (standard…py:467-470): one wave, launched only when it can fire.
-__global__ __launch_bounds__(64) void k_converge(const double* __restrict__ loss_hist, int64_t hist_base,
-                                                 int64_t iter, int64_t patience, double tol,
-                                                 int32_t* __restrict__ stop) {
-  if (*stop != 0 || threadIdx.x != 0) return;
-  const int64_t s = iter - patience;             // loss_running[ii - patience:]
-  const int64_t cnt = hist_base + iter - s;      // number of diffs in the slice
-  const double d = np_pairwise_sum_absdiff(loss_hist + s, cnt);
-  if (d < tol) *stop = (int32_t)(iter + 1);  // iterations completed (loss_running length)
-}
-
 }  // namespace tr
 
 // ==========================================================================================
@@ -1503,12 +1320,6 @@ hipError_t launch_cols_wide(int C, int W, int64_t nstripes, int64_t nchunks, con
   return hipSuccess;
 }
 
-hipError_t launch_converge(const double* loss_hist, int64_t hist_base, int64_t iter, int64_t patience, double tol,
-                           int32_t* stop, hipStream_t st) {
-  hipLaunchKernelGGL(k_converge, dim3(1), dim3(64), 0, st, loss_hist, hist_base, iter, patience, tol, stop);
-  return hipGetLastError();
-}
-
 // ---- slab reduction --------------------------------------------------------------------------
 hipError_t launch_reduce_slabs(int W, const float* part, int64_t nslabs, int64_t ncols, float* out,
                                const double* dpart, int64_t nd, double loss_scale, float* loss_slot,
@@ -1561,6 +1372,7 @@ static hipError_t mttkrp_launch_r(const FactorSet& fs, const float* phi, const f
 
 hipError_t launch_mttkrp(const FactorSet& fs, const float* phi, const float* dphi, const float* w,
                          const float* G, float* grad, const int32_t* stop, hipStream_t st) {
+  if (mttkrp2_supported(fs)) return launch_mttkrp2(fs, phi, dphi, w, G, grad, stop, st);
   int64_t rows = 0;
   for (int f = 0; f < fs.nf; ++f) rows += fs.dim[f];
   const int64_t padded = rows * (fs.rank | 1);  // odd LDS row stride (k_mttkrp)
@@ -1571,33 +1383,6 @@ hipError_t launch_mttkrp(const FactorSet& fs, const float* phi, const float* dph
   if (fs.rank <= 16) return mttkrp_launch_r<16>(fs, phi, dphi, w, G, grad, use_lds, stop, st, grid, lds);
   if (fs.rank <= 32) return mttkrp_launch_r<32>(fs, phi, dphi, w, G, grad, use_lds, stop, st, grid, lds);
   return mttkrp_launch_r<64>(fs, phi, dphi, w, G, grad, use_lds, stop, st, grid, lds);
-}
-
-bool update_prepare_mode_ok(const FactorSet& fs, int mode) {
-  // mode 1 only: the new factors are staged in the update workgroup's LDS.  (Building dense B
-  // there too was measured slower than the separate multi-workgroup k_build_dense: one CU took
-  // 17 us for config 2's 32768 x 8 products.)
-  return mode <= 0 || (mode == 1 && fs.nfelem * 4 <= 48 * 1024);
-}
-
-hipError_t launch_update(const FactorSet& fs, int n_bias, float* params, const float* grad,
-                         const UpdateArgs& ua, float* m, float* v, float* vmax, float* grad_total_out,
-                         float* loss_out, double* loss_hist, int32_t* stop, hipStream_t st, const PrepArgs* pa) {
-  PrepArgs p0;
-  std::memset(&p0, 0, sizeof(p0));
-  const PrepArgs& pp = pa != nullptr && ua.mode == 0 ? *pa : p0;
-  if (!update_prepare_mode_ok(fs, pp.mode)) return hipErrorInvalidValue;
-  const size_t lds = pp.mode > 0 ? (size_t)fs.nfelem * 4 : 0;
-  hipLaunchKernelGGL(k_update, dim3(1), dim3(1024), lds, st, fs, n_bias, params, grad, ua, m, v, vmax,
-                     grad_total_out, loss_out, loss_hist, stop, pp);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  if (ua.mode == 0 && loss_hist != nullptr && stop != nullptr && ua.iter > ua.patience && ua.tol > 0.0) {
-    hipLaunchKernelGGL(k_converge, dim3(1), dim3(64), 0, st, loss_hist, ua.hist_base, ua.iter, ua.patience,
-                       ua.tol, stop);
-    e = hipGetLastError();
-  }
-  return e;
 }
 
 }  // namespace tr
