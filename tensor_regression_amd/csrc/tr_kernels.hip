@@ -97,10 +97,13 @@ __global__ __launch_bounds__(256) void k_build_dense(FactorSet fs, const float* 
   const float* F = phi;
   if (use_lds) {
     const bool publish = blockIdx.x == 0;
-    for (int64_t k = threadIdx.x; k < fs.nfelem; k += blockDim.x) {
-      const float a = params[k];
+    unsigned nnmask = 0;  // factors under softplus
+#pragma unroll
+    for (int g = 0; g < TR_MAXF; ++g)
+      if (g < fs.nf && fs.nonneg[g]) nnmask |= 1u << g;
+    auto stage = [&](int64_t k, float a) {
       float v = a, d = 1.0f;
-      if (fs.nonneg[tr_factor_of(fs, k)]) {
+      if ((nnmask >> tr_factor_of(fs, k)) & 1u) {
         v = tr_softplus(a, beta, thr);
         d = tr_softplus_grad(a, beta, thr);
       }
@@ -109,7 +112,19 @@ __global__ __launch_bounds__(256) void k_build_dense(FactorSet fs, const float* 
         phi[k] = v;
         dphi[k] = d;
       }
+    };
+    // four elements per trip with their loads in flight together: the factors are read from a
+    // cold L2 right after the update, one round trip per element would dominate the launch
+    const int64_t B = blockDim.x;
+    int64_t k = threadIdx.x;
+    for (; k + 3 * B < fs.nfelem; k += 4 * B) {
+      const float a0 = params[k], a1 = params[k + B], a2 = params[k + 2 * B], a3 = params[k + 3 * B];
+      stage(k, a0);
+      stage(k + B, a1);
+      stage(k + 2 * B, a2);
+      stage(k + 3 * B, a3);
     }
+    for (; k < fs.nfelem; k += B) stage(k, params[k]);
     __syncthreads();
     F = sphi;
   }
@@ -118,11 +133,22 @@ __global__ __launch_bounds__(256) void k_build_dense(FactorSet fs, const float* 
        e += (int64_t)gridDim.x * blockDim.x) {
     int64_t idx[TR_MAXF];
     int64_t pos = 0;
+    if (fs.total < (int64_t(1) << 31)) {  // 32-bit index arithmetic (every config)
+      const uint32_t e32 = (uint32_t)e;
 #pragma unroll
-    for (int f = 0; f < TR_MAXF; ++f) {
-      if (f < fs.nf) {
-        idx[f] = (e / fs.rstride[f]) % fs.dim[f];
-        pos += idx[f] * fs.stride[f];
+      for (int f = 0; f < TR_MAXF; ++f) {
+        if (f < fs.nf) {
+          idx[f] = (e32 / (uint32_t)fs.rstride[f]) % (uint32_t)fs.dim[f];
+          pos += idx[f] * fs.stride[f];
+        }
+      }
+    } else {
+#pragma unroll
+      for (int f = 0; f < TR_MAXF; ++f) {
+        if (f < fs.nf) {
+          idx[f] = (e / fs.rstride[f]) % fs.dim[f];
+          pos += idx[f] * fs.stride[f];
+        }
       }
     }
     float s = 0.0f;

@@ -40,6 +40,10 @@ __device__ int g_upd_launch;
 
 namespace {
 constexpr int UPD_T = 1024;  // threads of the one workgroup (the norm order above assumes it)
+#ifndef TR_UPD_TRIP
+#define TR_UPD_TRIP 2
+#endif
+constexpr int UPD_TRIP = TR_UPD_TRIP;  // elements per thread per loop trip (loads in flight together)
 
 __device__ __forceinline__ int factor_of(const FactorSet& fs, int64_t e) {
   int f = 0;
@@ -134,12 +138,14 @@ __global__ __launch_bounds__(UPD_T) void k_update(FactorSet fs, int n_bias,
     for (int g = 0; g < TR_MAXF; ++g) accn[g] = g == f ? fmaf(a, a, accn[g]) : accn[g];
   };
   int64_t k = t;
-  for (; k + B < nfe; k += 2 * B) {
-    const float a0 = params[k], a1 = params[k + B];
-    acc(k, a0);
-    acc(k + B, a1);
+  for (; k + (UPD_TRIP - 1) * B < nfe; k += UPD_TRIP * B) {
+    float a[UPD_TRIP];
+#pragma unroll
+    for (int u = 0; u < UPD_TRIP; ++u) a[u] = params[k + u * B];
+#pragma unroll
+    for (int u = 0; u < UPD_TRIP; ++u) acc(k + u * B, a[u]);
   }
-  if (k < nfe) acc(k, params[k]);
+  for (; k < nfe; k += B) acc(k, params[k]);
 #pragma unroll
   for (int f = 0; f < TR_MAXF; ++f) {
     if (f < fs.nf) {
@@ -194,17 +200,23 @@ __global__ __launch_bounds__(UPD_T) void k_update(FactorSet fs, int n_bias,
       pa.dphi[e] = soft ? tr_softplus_grad(p, pa.beta, pa.thr) : 1.0f;
     }
   };
-  // two elements per trip: both elements' loads are in flight before either is consumed
+  // UPD_TRIP elements per trip: their loads are in flight before any is consumed
   int64_t e = t;
-  for (; e + B < np; e += 2 * B) {
-    const float g0 = grad[e], g1 = grad[e + B], p0 = params[e], p1 = params[e + B];
-    const float m0 = adam ? m[e] : 0.f, m1 = adam ? m[e + B] : 0.f;
-    const float v0 = adam ? v[e] : 0.f, v1 = adam ? v[e + B] : 0.f;
-    const float x0 = ams ? vmax[e] : 0.f, x1 = ams ? vmax[e + B] : 0.f;
-    step(e, g0, p0, m0, v0, x0);
-    step(e + B, g1, p1, m1, v1, x1);
+  for (; e + (UPD_TRIP - 1) * B < np; e += UPD_TRIP * B) {
+    float g[UPD_TRIP], p[UPD_TRIP], mo[UPD_TRIP], vo[UPD_TRIP], xo[UPD_TRIP];
+#pragma unroll
+    for (int u = 0; u < UPD_TRIP; ++u) {
+      const int64_t eu = e + u * B;
+      g[u] = grad[eu];
+      p[u] = params[eu];
+      mo[u] = adam ? m[eu] : 0.f;
+      vo[u] = adam ? v[eu] : 0.f;
+      xo[u] = ams ? vmax[eu] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < UPD_TRIP; ++u) step(e + u * B, g[u], p[u], mo[u], vo[u], xo[u]);
   }
-  if (e < np) step(e, grad[e], params[e], adam ? m[e] : 0.f, adam ? v[e] : 0.f, ams ? vmax[e] : 0.f);
+  for (; e < np; e += B) step(e, grad[e], params[e], adam ? m[e] : 0.f, adam ? v[e] : 0.f, ams ? vmax[e] : 0.f);
   UPD_MARK(3);
   if (t == 0) {
     float l2 = 0.f;

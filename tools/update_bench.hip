@@ -19,7 +19,12 @@
 #include <vector>
 
 #include "tr_common.h"
-#define TR_UPD_PROFILE 1
+#ifndef TR_UPD_PROFILE
+#define TR_UPD_PROFILE 0
+#endif
+#ifndef TR_UPD_TRIP
+#define TR_UPD_TRIP 2
+#endif
 #include "tr_update.hip"  // the library kernel (v5)
 
 #define CK(x)                                                                       \
@@ -489,6 +494,7 @@ int main() {
           CK(hipEventElapsedTime(&ms, a, b));
           if (r >= 5) tot += ms;
         }
+#if TR_UPD_PROFILE
         if (kv == 10) {
           long long prof[64][8];
           CK(hipMemcpyFromSymbol(prof, HIP_SYMBOL(tr::g_upd_prof), sizeof(prof)));
@@ -498,6 +504,7 @@ int main() {
           std::printf("%s v5 phases (ns from entry, mean of 40): norms-issued+reduced %.0f  synced %.0f  updated %.0f  "
                       "loss %.0f  end %.0f\n", c.name, acc[1] / 40, acc[2] / 40, acc[3] / 40, acc[4] / 40, acc[5] / 40);
         }
+#endif
         if (kv == 10 || kv == 4 || kv == 8 || kv == 9 || kv == 0) {  // warm-cache relaunches (kernel trace only): same kernel 20x back to back
           for (int r = 0; r < 20; ++r) {
             if (kv != 10) {
