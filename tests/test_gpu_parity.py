@@ -750,3 +750,40 @@ def test_kat1_notebook_trace_on_gpu():
     np.testing.assert_allclose(m.loss_running, rep["kat1_loss_running"], rtol=1e-6)
     n = min(len(m.loss_running), len(KAT1_TRACE))
     assert np.max(np.abs(np.array(m.loss_running[:n]) - KAT1_TRACE[:n]) / np.abs(KAT1_TRACE[:n])) <= 2 * rep["kat1_max_rel"]
+
+
+def test_kernel_timing_records_and_sampling():
+    """tr_plan_set_timing / tr_plan_set_timing_every / tr_plan_read_timing (measurement support
+    used by bench.py): every launch of a timed kind is recorded, or only every n-th one, and
+    timing does not change the fit (the events are stream-ordered markers only)."""
+    from tensor_regression_amd import CP_linear_regression
+    torch.manual_seed(3)
+    X = torch.randn(4096, 64, 32, device=DEV)
+    y = torch.randn(4096, device=DEV)
+    init = [torch.randn(d, 4, device=DEV) * 0.3 for d in (64, 32)]
+
+    def fit(every):
+        m = CP_linear_regression(X.shape, rank=4, device=DEV, Bcp_init=[a.clone().requires_grad_(True) for a in init],
+                                 bias_init=0.1)
+        m.fit_Adam(X, y, lambda_L2=0.01, max_iter=1, tol=0, patience=10, Adam_kwargs={"lr": 0.01})  # plan + warm-up
+        plan = m._plan
+        plan.read_timing()
+        if every:
+            plan.set_timing(True, kinds=["stream_fused"], every=every)
+        m.fit_Adam(X, y, lambda_L2=0.01, max_iter=12, tol=0, patience=10, Adam_kwargs={"lr": 0.01})
+        torch.cuda.synchronize()
+        kt = plan.read_timing()
+        plan.set_timing(False)
+        return kt, list(m.loss_running), [a.detach().cpu() for a in m.Bcp]
+
+    kt0, lr0, f0 = fit(0)
+    kt1, lr1, f1 = fit(1)
+    kt5, lr5, f5 = fit(5)
+    assert kt0["stream_fused"][1] == 0
+    assert kt1["stream_fused"][1] == 12 and kt1["stream_fused"][0] > 0.0
+    assert kt5["stream_fused"][1] == 2  # launches 5 and 10 of 12
+    assert all(kt1[k][1] == 0 for k in kt1 if k != "stream_fused")
+    # bitwise the same fit with and without the timing events
+    assert lr0 == lr1 == lr5
+    for a, b, c in zip(f0, f1, f5):
+        assert torch.equal(a, b) and torch.equal(a, c)
