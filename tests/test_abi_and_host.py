@@ -167,3 +167,39 @@ def test_spectral_constructor_matches_reference_init(name):
     np.testing.assert_array_equal(got_c, d["Bcp_c0"])
     assert [tuple(a.shape) for a in model.Bcp_c] == [tuple(s) for s in m["factor_shapes_c"]]
     assert model.bias.shape == (m["n_out"],) and all(a.requires_grad for a in model.Bcp_n + model.Bcp_c)
+
+
+def test_rccl_unique_id_bytes_roundtrip():
+    """The gradient all-reduce's RCCL communicator is bootstrapped from an ncclUniqueId that rank 0
+    broadcasts as raw bytes: ids with NUL bytes (binary) must survive the round trip whole."""
+    from tensor_regression_amd import _engine
+    raw = bytes([0, 7, 0, 255] * 32)
+    uid = _engine.uid_from_bytes(raw)
+    assert _engine.uid_to_bytes(uid) == raw
+    assert _engine.uid_to_bytes(_engine.uid_from_bytes(bytearray(raw))) == raw
+    with pytest.raises(ValueError):
+        _engine.uid_from_bytes(raw[:127])
+
+
+def test_gradient_allreduce_falls_back_to_torch_for_gloo():
+    """gloo groups (the CPU multi-process tests) keep torch.distributed.all_reduce; the direct
+    ncclAllReduce path is only taken for an NCCL (RCCL) group."""
+    import socket
+    import torch
+    import torch.distributed as dist
+    from tensor_regression_amd import _engine
+    if dist.is_initialized():
+        pytest.skip("a process group is already initialised in this process")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        ar = _engine.gradient_allreduce(dist.group.WORLD, 0)
+        assert not isinstance(ar, _engine.RcclAllReduce)
+        t = torch.arange(5, dtype=torch.float32)
+        ar(t)
+        assert torch.equal(t, torch.arange(5, dtype=torch.float32))
+    finally:
+        dist.destroy_process_group()

@@ -16,6 +16,7 @@ for cfg in "$@"; do
     c3) alg=2148007936; dom=k_mnl_duo ;;
     c4) alg=8590000128; dom=k_linear_cluster ;;
     c5) alg=4328783872; dom=k_spec_slice ;;
+    c6) alg=8590196736; dom=k_linear_fused ;;  # windowed: window bytes (overlapping rows hit L2 / MALL)
     c7) alg=1073774592; dom=k_linear_fused ;;  # HostStream: one launch per 8192-sample chunk
     *) alg=""; dom=k_linear_fused ;;
   esac
