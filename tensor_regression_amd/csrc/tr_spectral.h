@@ -42,8 +42,9 @@ struct SpecGeom {
   int gKP;  // K padded to 16 (row stride of the T / dT staging buffer)
   // column-slice training kernel (tr_spectral_slice.hip) for the shapes it covers (config 5)
   int sl;                       // 1: SPEC_TRAIN runs k_spec_slice
+  int slSp;                     // its GEMMs: 0 f32 MFMA, 1 exact bf16x3 split (lin packed), 2 split (lin unpacked)
   int slDt, sl_Dp;              // rows d >= 128 (<= 2), rows of the phi(A1) / phi(C1) tables
-  int sl_oTail, sl_oEx, sl_oTP, sl_oPart, sl_oN1, sl_oLoss, sl_lds_floats;  // LDS carve (floats)
+  int sl_oTail, sl_oEx, sl_oTP, sl_oPart, sl_oN1, sl_oLoss, sl_oPF, sl_lds_floats;  // LDS carve (floats)
 };
 
 // Fills g; returns false (with a reason) when the shape is outside the kernels' envelope.

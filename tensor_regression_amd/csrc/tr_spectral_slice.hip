@@ -59,6 +59,10 @@
 #else
 #define SL_NT ""
 #endif
+#ifndef TR_SLICE_PF
+#define TR_SLICE_PF 2  // L2 prefetch of the next sample at the top of each sample: 64-line (8 KiB) dword
+                       // LDS-DMA pieces per wave into a discarded LDS line (2: the whole sample)
+#endif
 #ifndef TR_SLICE_PROFILE
 #define TR_SLICE_PROFILE 0  // profiling build: per-phase cycle counts of wave 0 of workgroups 0..255
 #endif
@@ -101,6 +105,56 @@ constexpr int SL_TAIL = 64;             // tail floats per wave (Dt <= 2 rows x 
 __device__ __forceinline__ sl_f4 sl_mfma(float a, float b, sl_f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
+
+// ---- exact three-term bf16 split (SP > 0) ---------------------------------------------------
+// x = x1 + x2 + x3 with x1 = x truncated to its top 8 significand bits, x2 = the top 8 bits of
+// the (exact) remainder, x3 = the rest (at most 8 significant bits: exactly a bf16).  A product
+// a.b is formed as the six cross terms of weight >= 2^-16 (a1b1, a1b2, a2b1, a1b3, a2b2, a3b1)
+// on v_mfma_f32_16x16x32_bf16 (16x the f32 MFMA rate); the dropped terms a2b3, a3b2, a3b3
+// weigh <= 2^-24 |ab|, i.e. the f32 rounding of the product itself.
+typedef __bf16 sl_bf8 __attribute__((ext_vector_type(8)));
+typedef uint32_t sl_u4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ sl_f4 sl_mfma_bf(sl_u4 a, sl_u4 b, sl_f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(sl_bf8, a), __builtin_bit_cast(sl_bf8, b), c, 0,
+                                                 0, 0);
+}
+// split a (element 2m) and b (element 2m+1) into the three packed bf16 pairs of VGPR m
+__device__ __forceinline__ void sl_split2(float a, float b, uint32_t& h1, uint32_t& h2, uint32_t& h3) {
+  const uint32_t ua = __float_as_uint(a), ub = __float_as_uint(b);
+  h1 = __builtin_amdgcn_perm(ub, ua, 0x07060302u);
+  const float ra = a - __uint_as_float(ua & 0xffff0000u), rb = b - __uint_as_float(ub & 0xffff0000u);
+  const uint32_t ura = __float_as_uint(ra), urb = __float_as_uint(rb);
+  h2 = __builtin_amdgcn_perm(urb, ura, 0x07060302u);
+  const float sa = ra - __uint_as_float(ura & 0xffff0000u), sb = rb - __uint_as_float(urb & 0xffff0000u);
+  h3 = __builtin_amdgcn_perm(__float_as_uint(sb), __float_as_uint(sa), 0x07060302u);
+}
+__device__ __forceinline__ void sl_split_m(float a, float b, sl_u4 (&f)[3], int m) {
+  uint32_t h1, h2, h3;
+  sl_split2(a, b, h1, h2, h3);
+  f[0][m] = h1;
+  f[1][m] = h2;
+  f[2][m] = h3;
+}
+// c += A.B over the six cross terms (A, B each as three split fragments)
+__device__ __forceinline__ sl_f4 sl_mfma6(const sl_u4 (&a)[3], const sl_u4 (&b)[3], sl_f4 c) {
+  c = sl_mfma_bf(a[2], b[0], c);
+  c = sl_mfma_bf(a[1], b[1], c);
+  c = sl_mfma_bf(a[0], b[2], c);
+  c = sl_mfma_bf(a[1], b[0], c);
+  c = sl_mfma_bf(a[0], b[1], c);
+  c = sl_mfma_bf(a[0], b[0], c);
+  return c;
+}
+// packed lin columns (Rn <= 8): B = [b1 | b2] (lanes 0-7 | 8-15) and [b3 | 0]; column c of the
+// product is the sum of accumulator columns c and c + 8 (folded by sl_fold8): four MFMAs for
+// the six cross terms (a3b2 comes along)
+__device__ __forceinline__ sl_f4 sl_mfma_lp(const sl_u4 (&a)[3], const sl_u4 (&b)[2], sl_f4 c) {
+  c = sl_mfma_bf(a[2], b[0], c);
+  c = sl_mfma_bf(a[0], b[1], c);
+  c = sl_mfma_bf(a[1], b[0], c);
+  c = sl_mfma_bf(a[0], b[0], c);
+  return c;
+}
 template <int CTRL>
 __device__ __forceinline__ float sl_dpp(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
@@ -124,6 +178,8 @@ __device__ __forceinline__ float sl_xor32(float v) {
   return __uint_as_float(q[0]) + __uint_as_float(q[1]);
 }
 __device__ __forceinline__ float sl_groups_sum(float v) { return sl_xor32(sl_xor16(v)); }
+// lanes i and i ^ 8 of each 16-lane row summed (row_ror:8); both end with the same value
+__device__ __forceinline__ float sl_fold8(float v) { return v + sl_dpp<0x128>(v); }
 // barrier that leaves LDS-DMA in flight (__syncthreads() would wait vmcnt(0))
 __device__ __forceinline__ void sl_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -168,7 +224,9 @@ __device__ __forceinline__ void sl_wait_vm(int n) {
 __device__ __forceinline__ int sl_swz(int x) { return (x & 1) | ((x & 2) << 1); }
 }  // namespace
 
-template <int CC, int DT>
+// SP: 0 = both GEMMs on v_mfma_f32_16x16x4_f32; 1 = exact three-term bf16 split on
+// v_mfma_f32_16x16x32_bf16 with the lin columns packed (Rn <= 8); 2 = split, lin unpacked
+template <int CC, int DT, int SP>
 __global__ __launch_bounds__(SL_T) void k_spec_slice(
     const float* __restrict__ X, int64_t N, int64_t xld, SpecGeom g, const float* __restrict__ phi,
     const float* __restrict__ Phi0, const float* __restrict__ wts, const float* __restrict__ y, float scale,
@@ -224,12 +282,39 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
 
   // B fragments: lane (i, gq) of step s holds Phi0[wbase + 4 s + gq, column]; tile 0 column i is
   // spectral column i (Phi0 column Rn + i), tile 1 column i is lin column i
-  float bf0[SL_STEPS], bf1[SL_STEPS];
+  constexpr int NS = SP ? 1 : SL_STEPS;
+  float bf0[NS], bf1[NS];
+  // split mode: k step S covers steps 8S .. 8S+7 (element j of lane group gq <-> w = 32 S + 4 j
+  // + gq of the half, the same w for A and B); bs = spectral columns, bl = lin columns
+  constexpr int NSP = SP ? SL_STEPS / 8 : 1;
+  constexpr int NL = SP == 2 ? 3 : 2;
+  sl_u4 bs[NSP][3], bl[NSP][NL];
+  if constexpr (!SP) {
 #pragma unroll
-  for (int s = 0; s < SL_STEPS; ++s) {
-    const int64_t w = wbase + 4 * s + gq;
-    bf0[s] = i < RC ? Phi0[w * K + Rn + i] : 0.f;
-    bf1[s] = i < Rn ? Phi0[w * K + i] : 0.f;
+    for (int s = 0; s < NS; ++s) {
+      const int64_t w = wbase + 4 * s + gq;
+      bf0[s] = i < RC ? Phi0[w * K + Rn + i] : 0.f;
+      bf1[s] = i < Rn ? Phi0[w * K + i] : 0.f;
+    }
+  } else {
+    const int cl = SP == 1 ? (i & 7) : i;  // lin column this lane splits
+#pragma unroll
+    for (int S = 0; S < NSP; ++S)
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int64_t w0 = wbase + 4 * (8 * S + 2 * m) + gq, w1 = w0 + 4;
+        sl_split_m(i < RC ? Phi0[w0 * K + Rn + i] : 0.f, i < RC ? Phi0[w1 * K + Rn + i] : 0.f, bs[S], m);
+        uint32_t h1, h2, h3;
+        sl_split2(cl < Rn ? Phi0[w0 * K + cl] : 0.f, cl < Rn ? Phi0[w1 * K + cl] : 0.f, h1, h2, h3);
+        if constexpr (SP == 1) {
+          bl[S][0][m] = i < 8 ? h1 : h2;
+          bl[S][1][m] = i < 8 ? h3 : 0u;
+        } else {
+          bl[S][0][m] = h1;
+          bl[S][1][m] = h2;
+          bl[S][NL - 1][m] = h3;
+        }
+      }
   }
   sl_f4 gacc[SL_TILES][2];
 #pragma unroll
@@ -284,8 +369,10 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
     dma_piece(n, q, 1);
   };
   auto dma_tail = [&](int64_t n) {
-    if (lane < Dt * TR) {  // lane -> (row 128 + lane / TR, w offset lane % TR)
-      const int tr = lane / TR, wo = lane - tr * TR;
+    int ln = lane;  // opaque copy: the per-lane source is formed at the call (no live address pair)
+    asm volatile("" : "+v"(ln));
+    if (ln < Dt * TR) {  // lane -> (row 128 + lane / TR, w offset lane % TR)
+      const int tr = ln / TR, wo = ln - tr * TR;
       const int64_t w = wbase + TR * p + wo;
       sl_dma4(X + n * xld + w * D + 128 + tr, sTail);
     }
@@ -298,6 +385,24 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
 
   __builtin_amdgcn_s_waitcnt(0);  // retire the prologue's loads (the loop's waits are counted)
   __syncthreads();
+  // L2 prefetch of sample n: wave wv touches the 128-B lines (2 wv + pc) * 64 + lane, pc < TR_SLICE_PF,
+  // of the sample's W * D floats (one dword each, landing in a shared scratch LDS line that nothing
+  // reads): the sample's HBM transfer then overlaps this sample's forward and epilogue, and its
+  // LDS-DMA in the gradient GEMM reads L2.  (The LDS holds one sample: without it the next
+  // sample's transfer could only overlap the gradient GEMM.)
+  constexpr int NPF = TR_SLICE_PF;
+  auto prefetch = [&](int64_t n) {
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int64_t sbytes = (int64_t)g.W * D * 4;
+    const char* base = reinterpret_cast<const char*>(X + n * xld);
+#pragma unroll
+    for (int pc = 0; pc < NPF; ++pc) {
+      int64_t off = ((int64_t)((2 * wv + pc) * 64 + ln)) * 128;
+      off = off < sbytes ? off : sbytes - 4;
+      sl_dma4(reinterpret_cast<const float*>(base + off), lds + g.sl_oPF);
+    }
+  };
   if (nr > 0) dma_sample(sample_of(0));
   if (TR_SLICE_PRIO && hw == 1) __builtin_amdgcn_s_setprio(1);
 #if TR_SLICE_PROFILE
@@ -310,17 +415,22 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
     const int64_t n = sample_of(k);
     const bool has_next = k + 1 < nr && !((TR_SLICE_SKIP & 1) && k > 0);
     const int64_t nn = has_next ? sample_of(k + 1) : n;
+    // pieces issued below this sample's DMA (the forward's counted waits allow for them)
+    const int npf = (NPF > 0 && has_next) ? NPF : 0;
+    if (npf > 0) prefetch(nn);
 
     // ---- forward: T (tile jt, d tile h) over this wave's half ---------------------------
     sl_f4 T00 = {0.f, 0.f, 0.f, 0.f}, T01 = T00, T10 = T00, T11 = T00;
     // tail rows d = 128 + tr: VALU partial over this wave's tail steps [SQ p, SQ (p + 1)) inside
     // the forward loop (bf0 / bf1 of the step are in hand), reduced over lane groups after it
     float ta[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
+    sl_f4 Tts = {0.f, 0.f, 0.f, 0.f}, Ttl = Tts;  // split mode: tail rows (row tr = lane group 0, reg tr)
     {
       sl_f2 xa[4], xb[4];
+      sl_u4 xf[2][3];  // split mode: the k step's A fragments of d tiles 0 / 1
       {
         SL_SUB_BEGIN();
-        sl_wait_vm((ntl - 1) * 2);
+        sl_wait_vm((ntl - 1) * 2 + npf);
         SL_SUB_END(1);
       }
 #pragma unroll
@@ -330,29 +440,52 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
         if (q + 1 < ntl) {
           {
             SL_SUB_BEGIN();
-            sl_wait_vm((ntl - 2 - q) * 2);
+            sl_wait_vm((ntl - 2 - q) * 2 + npf);
             SL_SUB_END(1);
           }
 #pragma unroll
           for (int s = 0; s < 4; ++s)
             xb[s] = *reinterpret_cast<const sl_f2*>(slice + 128 * (4 * (q + 1) + s) + fo[s]);
         }
+        if constexpr (!SP) {
 #pragma unroll
-        for (int s = 0; s < 4 && !(TR_SLICE_SKIP & 2); ++s) {
-          T00 = sl_mfma(xa[s].x, bf0[4 * q + s], T00);
-          T01 = sl_mfma(xa[s].y, bf0[4 * q + s], T01);
-          T10 = sl_mfma(xa[s].x, bf1[4 * q + s], T10);
-          T11 = sl_mfma(xa[s].y, bf1[4 * q + s], T11);
+          for (int s = 0; s < 4 && !(TR_SLICE_SKIP & 2); ++s) {
+            T00 = sl_mfma(xa[s].x, bf0[4 * q + s], T00);
+            T01 = sl_mfma(xa[s].y, bf0[4 * q + s], T01);
+            T10 = sl_mfma(xa[s].x, bf1[4 * q + s], T10);
+            T11 = sl_mfma(xa[s].y, bf1[4 * q + s], T11);
+          }
+        } else {
+          // tile q holds elements 4 (q & 1) .. +3 of k step q / 2: VGPRs 2 (q & 1), 2 (q & 1) + 1
+#pragma unroll
+          for (int mm = 0; mm < 2; ++mm) {
+            sl_split_m(xa[2 * mm].x, xa[2 * mm + 1].x, xf[0], 2 * (q & 1) + mm);
+            sl_split_m(xa[2 * mm].y, xa[2 * mm + 1].y, xf[1], 2 * (q & 1) + mm);
+          }
+          if ((q & 1) && !(TR_SLICE_SKIP & 2)) {
+            const int S = q >> 1;
+            T00 = sl_mfma6(xf[0], bs[S], T00);
+            T01 = sl_mfma6(xf[1], bs[S], T01);
+            if constexpr (SP == 1) {
+              T10 = sl_mfma_lp(xf[0], bl[S], T10);
+              T11 = sl_mfma_lp(xf[1], bl[S], T11);
+            } else {
+              T10 = sl_mfma6(xf[0], bl[S], T10);
+              T11 = sl_mfma6(xf[1], bl[S], T11);
+            }
+          }
         }
-        if (Dt > 0 && q / TQ == p) {
+        if constexpr (!SP) {
+          if (Dt > 0 && q / TQ == p) {
 #pragma unroll
-          for (int s = 0; s < 4; ++s) {
-            const int wo = 4 * (4 * q + s - SQ * p) + gq;
+            for (int s = 0; s < 4; ++s) {
+              const int wo = 4 * (4 * q + s - SQ * p) + gq;
 #pragma unroll
-            for (int tr = 0; tr < Dt; ++tr) {
-              const float xt = sTail[tr * TR + wo];
-              ta[tr][0] = fmaf(xt, bf0[4 * q + s], ta[tr][0]);
-              ta[tr][1] = fmaf(xt, bf1[4 * q + s], ta[tr][1]);
+              for (int tr = 0; tr < Dt; ++tr) {
+                const float xt = sTail[tr * TR + wo];
+                ta[tr][0] = fmaf(xt, bf0[4 * q + s], ta[tr][0]);
+                ta[tr][1] = fmaf(xt, bf1[4 * q + s], ta[tr][1]);
+              }
             }
           }
         }
@@ -360,11 +493,59 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
         for (int s = 0; s < 4; ++s) xa[s] = xb[s];
       }
     }
+    // lane-dependent indices of the epilogue from an opaque copy of the lane index: every LDS
+    // address below is then formed here (a few VALU ops) instead of living across the loop
+    // (held through the GEMMs, the split kernels spilled them to scratch: a vmcnt(0) reload each)
+    int lk = lane;
+    asm volatile("" : "+v"(lk));
+    const int i = lk & 15, gq = lk >> 4;
+    const int rs = i / CC;
+    const bool rs_ok = rs < Rs;
+    const bool vlane = rs_ok && (i % CC) == 0;
+    if constexpr (SP == 1) {  // packed lin columns: column c = accumulator columns c + (c ^ 8)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        T10[v] = sl_fold8(T10[v]);
+        T11[v] = sl_fold8(T11[v]);
+      }
+    }
+    if constexpr (SP) {
+      if (Dt > 0) {
+        // tail rows d = 128 + tr over this wave's tail k step (S = p): A row i = tail row i
+        // (rows >= Dt zero), element j <-> w offset 4 j + gq of the wave's 32 tail w (after the
+        // loop: nothing of the forward is live; one case per static S)
+        sl_u4 tf[3];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const float x0 = i < Dt ? sTail[i * TR + 8 * m + gq] : 0.f;
+          const float x1 = i < Dt ? sTail[i * TR + 8 * m + 4 + gq] : 0.f;
+          sl_split_m(x0, x1, tf, m);
+        }
+        auto tail_step = [&](const sl_u4(&b_s)[3], const sl_u4(&b_l)[NL]) {
+          Tts = sl_mfma6(tf, b_s, Tts);
+          if constexpr (SP == 1)
+            Ttl = sl_mfma_lp(tf, b_l, Ttl);
+          else
+            Ttl = sl_mfma6(tf, b_l, Ttl);
+        };
+        switch (p) {
+          case 0: tail_step(bs[0], bl[0]); break;
+          case 1: tail_step(bs[1], bl[1]); break;
+          case 2: tail_step(bs[2], bl[2]); break;
+          default: tail_step(bs[3], bl[3]); break;
+        }
+      }
+    }
     if (Dt > 0) {
 #pragma unroll
       for (int tr = 0; tr < Dt; ++tr) {
-        ta[tr][0] = sl_groups_sum(ta[tr][0]);
-        ta[tr][1] = sl_groups_sum(ta[tr][1]);
+        if constexpr (SP) {
+          ta[tr][0] = Tts[tr];
+          ta[tr][1] = SP == 1 ? sl_fold8(Ttl[tr]) : Ttl[tr];
+        } else {
+          ta[tr][0] = sl_groups_sum(ta[tr][0]);
+          ta[tr][1] = sl_groups_sum(ta[tr][1]);
+        }
         if (gq == 0) {
           sTP[(wv * 2 + tr) * 32 + i] = ta[tr][0];
           sTP[(wv * 2 + tr) * 32 + 16 + i] = ta[tr][1];
@@ -373,13 +554,13 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
     }
     SL_MARK(0);
     // ---- exchange the spectral tiles with the partner half ---------------------------------
-    *reinterpret_cast<sl_f4*>(sEx + (wv * TR_WAVE + lane) * 8) = T00;
-    *reinterpret_cast<sl_f4*>(sEx + (wv * TR_WAVE + lane) * 8 + 4) = T01;
+    *reinterpret_cast<sl_f4*>(sEx + (wv * TR_WAVE + lk) * 8) = T00;
+    *reinterpret_cast<sl_f4*>(sEx + (wv * TR_WAVE + lk) * 8 + 4) = T01;
     SL_MARK(2);
     sl_barrier();
     SL_MARK(3);
     {
-      const float* pe = sEx + ((wv ^ 4) * TR_WAVE + lane) * 8;
+      const float* pe = sEx + ((wv ^ 4) * TR_WAVE + lk) * 8;
       T00 += *reinterpret_cast<const sl_f4*>(pe);  // two-term sums commute: both halves hold
       T01 += *reinterpret_cast<const sl_f4*>(pe + 4);  // the bitwise-identical full tile
     }
@@ -394,11 +575,10 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
     }
 
     // y of this sample, lane o (n_out <= 64); read by readlane after barrier B
-    const float yv = lane < NO ? y[n * NO + lane] : 0.f;
 
     // ---- column partials: Z (lin, both d tiles, this half's partial T) and V (spectral, own d
     // tile h = hw, full T) -- nothing but the two sums stays live across barrier B -------------
-    auto norm_of = [&](float x) {  // || T[d, spectral group of this lane] ||
+    auto norm_of = [&](float x) {  // || T[d, spectral group of this lk] ||
       float sq = x * x;
       if (CC >= 2) sq += sl_dpp<0xB1>(sq);
       if (CC >= 4) sq += sl_dpp<0x4E>(sq);
@@ -406,7 +586,7 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
     };
     // table offsets from an opaque copy of the lane index: recomputed here (a few VALU ops)
     // instead of living across the sample loop as spilled registers
-    int lo = lane;
+    int lo = lk;
     asm volatile("" : "+v"(lo));
     const int ie = lo & 15, ge = lo >> 4, rse = ie / CC;
     // phi(A1)[d, ie] / phi(C1)[d, ie / CC] of this lane's 8 rows d = dbase + 8 ge + 2v + h: two
@@ -434,7 +614,7 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
     }
     vp = vlane ? vp : 0.f;
     const float Mt = norm_of(tt0);
-    const int dtl = 128 + gq;  // tail row of this lane group (valid when gq < Dt)
+    const int dtl = 128 + gq;  // tail row of this lk group (valid when gq < Dt)
     const float n1t = (Dt > 0 && gq < Dt && i < Rn) ? sN1[i * Dp + dtl] : 0.f;
     const float c1t = (Dt > 0 && gq < Dt && rs_ok) ? sC1[rs * Dp + dtl] : 0.f;
     zp = sl_groups_sum(zp);
@@ -471,14 +651,15 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
       const float ps = sl_row_sum16(cc * vi);
       const float b = sB[o];
       const float yh = (Rn > 0 ? pl + b : 0.f) + (Rs > 0 ? ps + b : 0.f);
-      const float e = yh - __int_as_float(__builtin_amdgcn_readlane(__float_as_int(yv), o));
+      // y by a scalar load (a vector load's compiler-inserted vmcnt(0) would drain the prefetch)
+      const float e = yh - y[n * NO + o];
       const float rv = e * scale;
       dz = fmaf(rv, ca, dz);
       dv = fmaf(rv, sCC[o * 16 + rs], dv);
-      if (wv == 0 && lane < 16) {
+      if (wv == 0 && lk < 16) {
         if (i < Rn) sAcc[o * Rn + i] += sWt[i] * rv * zi;
         if (i < Rs) sAcc[NO * Rn + o * Rs + i] += rv * vi;
-        if (lane == 0) {
+        if (lk == 0) {
           sAcc[NO * (Rn + Rs) + o] += bm * rv;
           *sLoss += (double)e * (double)e;
           if (out != nullptr) out[n * NO + o] = yh;
@@ -524,6 +705,26 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         dma_tail(nn);
       }
+      // split mode: B fragments of dT (element 2v + h of lane group g = d row 8g + 2v + h of the
+      // pair: spectral T0h[v], lin T1h[v])
+      sl_u4 ds[3], dl[NL];
+      if constexpr (SP) {
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          sl_split_m(T00[v], T01[v], ds, v);
+          uint32_t h1, h2, h3;
+          sl_split2(T10[v], T11[v], h1, h2, h3);
+          if constexpr (SP == 1) {  // lanes 8-15 take the second part of column i - 8
+            const uint32_t h2r = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)h2, 0x128, 0xF, 0xF, false);
+            dl[0][v] = i < 8 ? h1 : h2r;
+            dl[1][v] = i < 8 ? h3 : 0u;
+          } else {
+            dl[0][v] = h1;
+            dl[1][v] = h2;
+            dl[NL - 1][v] = h3;
+          }
+        }
+      }
       sl_f4 pa, pb;
       if (TR_SLICE_BPF) {
         pa = *reinterpret_cast<const sl_f4*>(slice + bo0);
@@ -546,20 +747,42 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
           }
           // the tile's two LDS-DMA pieces of the next sample go out between its MFMAs (after
           // the reads landed), not back to back: bursts stall on the memory issue queue
+          if constexpr (!SP) {
 #pragma unroll
-          for (int v = 0; v < 4; ++v) {
-            const sl_f4& src = v < 2 ? va : vb;
-            const float a0 = src[2 * (v & 1) + 0], a1 = src[2 * (v & 1) + 1];
-            if (!(TR_SLICE_SKIP & 4)) {
-              gacc[q][0] = sl_mfma(a0, T00[v], gacc[q][0]);
-              gacc[q][1] = sl_mfma(a0, T10[v], gacc[q][1]);
-              gacc[q][0] = sl_mfma(a1, T01[v], gacc[q][0]);
-              gacc[q][1] = sl_mfma(a1, T11[v], gacc[q][1]);
+            for (int v = 0; v < 4; ++v) {
+              const sl_f4& src = v < 2 ? va : vb;
+              const float a0 = src[2 * (v & 1) + 0], a1 = src[2 * (v & 1) + 1];
+              if (!(TR_SLICE_SKIP & 4)) {
+                gacc[q][0] = sl_mfma(a0, T00[v], gacc[q][0]);
+                gacc[q][1] = sl_mfma(a0, T10[v], gacc[q][1]);
+                gacc[q][0] = sl_mfma(a1, T01[v], gacc[q][0]);
+                gacc[q][1] = sl_mfma(a1, T11[v], gacc[q][1]);
+              }
+              if (has_next && (v & 1)) {
+                if (v == 1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // tile q's reads landed
+                // (with TR_SLICE_BPF the next tile's two reads may still be in flight: waited too)
+                dma_piece(nn, q, v >> 1);
+              }
             }
-            if (has_next && (v & 1)) {
-              if (v == 1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // tile q's reads landed
-              // (with TR_SLICE_BPF the next tile's two reads may still be in flight: waited too)
-              dma_piece(nn, q, v >> 1);
+          } else {
+            // A fragments: element 2v + h = X[w, d of (v, h)] (the order dT is held in)
+            sl_u4 af[3];
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+              const sl_f4& src = v < 2 ? va : vb;
+              sl_split_m(src[2 * (v & 1) + 0], src[2 * (v & 1) + 1], af, v);
+            }
+            if (has_next) {
+              asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // tile q's reads landed
+              dma_piece(nn, q, 0);
+            }
+            if (!(TR_SLICE_SKIP & 4)) gacc[q][0] = sl_mfma6(af, ds, gacc[q][0]);
+            if (has_next) dma_piece(nn, q, 1);
+            if (!(TR_SLICE_SKIP & 4)) {
+              if constexpr (SP == 1)
+                gacc[q][1] = sl_mfma_lp(af, dl, gacc[q][1]);
+              else
+                gacc[q][1] = sl_mfma6(af, dl, gacc[q][1]);
             }
           }
           if (Dt > 0 && q / TQ == p) {
@@ -578,6 +801,12 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
 #endif
   // ---- per-workgroup slab (arena layout, phi space) -------------------------------------------
   __syncthreads();  // (no LDS-DMA in flight: the last sample issued none)
+  if constexpr (SP == 1) {  // packed lin columns
+#pragma unroll
+    for (int q = 0; q < SL_TILES; ++q)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) gacc[q][1][v] = sl_fold8(gacc[q][1][v]);
+  }
 #pragma unroll
   for (int q = 0; q < SL_TILES; ++q)
 #pragma unroll
@@ -645,6 +874,9 @@ void spec_slice_geom(SpecGeom* g) {
   const int Dt = g->D > 128 ? g->D - 128 : 0;
   if (g->NO > 64) return;
   g->slDt = Dt;
+  // GEMMs on the bf16 matrix cores through the exact three-term split with TR_SLICE_SPLIT=1
+  const char* spl = std::getenv("TR_SLICE_SPLIT");
+  g->slSp = (spl != nullptr && spl[0] == '1') ? (g->Rn <= 8 ? 1 : 2) : 0;
   g->sl_Dp = ((g->D > 128 ? g->D : 128) + 3) & ~3;
   g->sl_oTail = SL_NW * SL_SLICE;
   g->sl_oEx = g->sl_oTail + SL_NW * SL_TAIL;
@@ -654,25 +886,30 @@ void spec_slice_geom(SpecGeom* g) {
   const int64_t small = (int64_t)g->sl_Dp * (g->Rn + g->Rs) + (int64_t)g->NO * 33 + 16 +
                         (int64_t)g->NO * (g->Rn + g->Rs + 1) + 2 * 32;
   g->sl_oLoss = (int)(g->sl_oN1 + ((small + 3) & ~(int64_t)3));  // 16-B aligned double
-  const int64_t tot = g->sl_oLoss + 4;
+  g->sl_oPF = g->sl_oLoss + 4;  // 64 floats: landing line of the L2 prefetch (never read)
+  const int64_t tot = g->sl_oPF + 64;
   if (tot * 4 > 160 * 1024) return;
   g->sl_lds_floats = (int)tot;
   g->sl = 1;
 }
 
-template <int DT>
+template <int DT, int SP>
 static const void* slice_kernel_dt(int cc) {
-  if (cc == 1) return reinterpret_cast<const void*>(&k_spec_slice<1, DT>);
-  if (cc == 2) return reinterpret_cast<const void*>(&k_spec_slice<2, DT>);
-  return reinterpret_cast<const void*>(&k_spec_slice<4, DT>);
+  if (cc == 1) return reinterpret_cast<const void*>(&k_spec_slice<1, DT, SP>);
+  if (cc == 2) return reinterpret_cast<const void*>(&k_spec_slice<2, DT, SP>);
+  return reinterpret_cast<const void*>(&k_spec_slice<4, DT, SP>);
 }
-static const void* slice_kernel(int cc, int dt) {
-  return dt == 0 ? slice_kernel_dt<0>(cc) : (dt == 1 ? slice_kernel_dt<1>(cc) : slice_kernel_dt<2>(cc));
+template <int SP>
+static const void* slice_kernel_sp(int cc, int dt) {
+  return dt == 0 ? slice_kernel_dt<0, SP>(cc) : (dt == 1 ? slice_kernel_dt<1, SP>(cc) : slice_kernel_dt<2, SP>(cc));
+}
+static const void* slice_kernel(int cc, int dt, int sp) {
+  return sp == 0 ? slice_kernel_sp<0>(cc, dt) : (sp == 1 ? slice_kernel_sp<1>(cc, dt) : slice_kernel_sp<2>(cc, dt));
 }
 
 hipError_t spec_slice_prepare(SpecGeom* g) {
   if (!g->sl) return hipSuccess;
-  const void* k = slice_kernel(g->Cc, g->slDt);
+  const void* k = slice_kernel(g->Cc, g->slDt, g->slSp);
   hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, g->sl_lds_floats * 4);
   if (e != hipSuccess) return e;
   int per_cu = 0;
@@ -687,26 +924,12 @@ hipError_t launch_spec_slice(const SpecGeom& g, int grid, const float* X, int64_
                              int64_t slab_stride, double* dpart, float* out, int64_t rows_per_wg, int reverse,
                              const int32_t* stop, hipStream_t st) {
   const size_t lb = (size_t)g.sl_lds_floats * 4;
-#define SL_LAUNCH(C, T)                                                                                          \
-  hipLaunchKernelGGL((k_spec_slice<C, T>), dim3(grid), dim3(SL_T), lb, st, X, N, xld, g, phi, Phi0, wts, y, scale, \
-                     slab, slab_stride, dpart, out, rows_per_wg, reverse, stop)
-#define SL_LAUNCH_CC(T) \
-  if (g.Cc == 1)        \
-    SL_LAUNCH(1, T);    \
-  else if (g.Cc == 2)   \
-    SL_LAUNCH(2, T);    \
-  else                  \
-    SL_LAUNCH(4, T);
-  if (g.slDt == 0) {
-    SL_LAUNCH_CC(0)
-  } else if (g.slDt == 1) {
-    SL_LAUNCH_CC(1)
-  } else {
-    SL_LAUNCH_CC(2)
-  }
-#undef SL_LAUNCH_CC
-#undef SL_LAUNCH
-  return hipGetLastError();
+  const void* k = slice_kernel(g.Cc, g.slDt, g.slSp);
+  void* args[] = {(void*)&X,    (void*)&N,     (void*)&xld,         (void*)&g,     (void*)&phi,
+                  (void*)&Phi0, (void*)&wts,   (void*)&y,           (void*)&scale, (void*)&slab,
+                  (void*)&slab_stride, (void*)&dpart, (void*)&out, (void*)&rows_per_wg, (void*)&reverse,
+                  (void*)&stop};
+  return hipLaunchKernel(k, dim3(grid), dim3(SL_T), args, lb, st);
 }
 
 #if TR_SLICE_PROFILE
