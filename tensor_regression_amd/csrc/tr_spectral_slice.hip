@@ -60,8 +60,14 @@
 #define SL_NT ""
 #endif
 #ifndef TR_SLICE_PF
-#define TR_SLICE_PF 2  // L2 prefetch of the next sample at the top of each sample: 64-line (8 KiB) dword
-                       // LDS-DMA pieces per wave into a discarded LDS line (2: the whole sample)
+#define TR_SLICE_PF 0  // split kernels: L2 prefetch of the next sample, dword LDS-DMA pieces per wave
+                       // (64 lanes at a TR_SLICE_PFS-byte stride) into a discarded LDS line
+#endif
+#ifndef TR_SLICE_PFS
+#define TR_SLICE_PFS 128  // prefetch stride (bytes); TR_SLICE_PF * 64 * 8 * stride covers the sample
+#endif
+#ifndef TR_SLICE_PFAT
+#define TR_SLICE_PFAT 0  // 0: prefetch at the top of the sample (before the forward), 1: after the forward
 #endif
 #ifndef TR_SLICE_PROFILE
 #define TR_SLICE_PROFILE 0  // profiling build: per-phase cycle counts of wave 0 of workgroups 0..255
@@ -118,8 +124,20 @@ __device__ __forceinline__ sl_f4 sl_mfma_bf(sl_u4 a, sl_u4 b, sl_f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(sl_bf8, a), __builtin_bit_cast(sl_bf8, b), c, 0,
                                                  0, 0);
 }
+#ifndef TR_SLICE_PK
+#define TR_SLICE_PK 0  // split remainders by packed-f32 subtractions (v_pk_add_f32)
+#endif
 // split a (element 2m) and b (element 2m+1) into the three packed bf16 pairs of VGPR m
 __device__ __forceinline__ void sl_split2(float a, float b, uint32_t& h1, uint32_t& h2, uint32_t& h3) {
+#if TR_SLICE_PK
+  const uint32_t ua = __float_as_uint(a), ub = __float_as_uint(b);
+  h1 = __builtin_amdgcn_perm(ub, ua, 0x07060302u);
+  const sl_f2 r = sl_f2{a, b} - sl_f2{__uint_as_float(ua & 0xffff0000u), __uint_as_float(ub & 0xffff0000u)};
+  const uint32_t ura = __float_as_uint(r.x), urb = __float_as_uint(r.y);
+  h2 = __builtin_amdgcn_perm(urb, ura, 0x07060302u);
+  const sl_f2 q = r - sl_f2{__uint_as_float(ura & 0xffff0000u), __uint_as_float(urb & 0xffff0000u)};
+  h3 = __builtin_amdgcn_perm(__float_as_uint(q.y), __float_as_uint(q.x), 0x07060302u);
+#else
   const uint32_t ua = __float_as_uint(a), ub = __float_as_uint(b);
   h1 = __builtin_amdgcn_perm(ub, ua, 0x07060302u);
   const float ra = a - __uint_as_float(ua & 0xffff0000u), rb = b - __uint_as_float(ub & 0xffff0000u);
@@ -127,6 +145,7 @@ __device__ __forceinline__ void sl_split2(float a, float b, uint32_t& h1, uint32
   h2 = __builtin_amdgcn_perm(urb, ura, 0x07060302u);
   const float sa = ra - __uint_as_float(ura & 0xffff0000u), sb = rb - __uint_as_float(urb & 0xffff0000u);
   h3 = __builtin_amdgcn_perm(__float_as_uint(sb), __float_as_uint(sa), 0x07060302u);
+#endif
 }
 __device__ __forceinline__ void sl_split_m(float a, float b, sl_u4 (&f)[3], int m) {
   uint32_t h1, h2, h3;
@@ -390,7 +409,7 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
   // reads): the sample's HBM transfer then overlaps this sample's forward and epilogue, and its
   // LDS-DMA in the gradient GEMM reads L2.  (The LDS holds one sample: without it the next
   // sample's transfer could only overlap the gradient GEMM.)
-  constexpr int NPF = TR_SLICE_PF;
+  constexpr int NPF = SP ? TR_SLICE_PF : 0;
   auto prefetch = [&](int64_t n) {
     int ln = lane;
     asm volatile("" : "+v"(ln));
@@ -398,7 +417,7 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
     const char* base = reinterpret_cast<const char*>(X + n * xld);
 #pragma unroll
     for (int pc = 0; pc < NPF; ++pc) {
-      int64_t off = ((int64_t)((2 * wv + pc) * 64 + ln)) * 128;
+      int64_t off = ((int64_t)((NPF * wv + pc) * 64 + ln)) * TR_SLICE_PFS;
       off = off < sbytes ? off : sbytes - 4;
       sl_dma4(reinterpret_cast<const float*>(base + off), lds + g.sl_oPF);
     }
@@ -416,7 +435,7 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
     const bool has_next = k + 1 < nr && !((TR_SLICE_SKIP & 1) && k > 0);
     const int64_t nn = has_next ? sample_of(k + 1) : n;
     // pieces issued below this sample's DMA (the forward's counted waits allow for them)
-    const int npf = (NPF > 0 && has_next) ? NPF : 0;
+    const int npf = (NPF > 0 && has_next && !TR_SLICE_PFAT) ? NPF : 0;
     if (npf > 0) prefetch(nn);
 
     // ---- forward: T (tile jt, d tile h) over this wave's half ---------------------------
@@ -493,6 +512,7 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
         for (int s = 0; s < 4; ++s) xa[s] = xb[s];
       }
     }
+    if (TR_SLICE_PFAT && NPF > 0 && has_next) prefetch(nn);
     // lane-dependent indices of the epilogue from an opaque copy of the lane index: every LDS
     // address below is then formed here (a few VALU ops) instead of living across the loop
     // (held through the GEMMs, the split kernels spilled them to scratch: a vmcnt(0) reload each)
@@ -874,9 +894,9 @@ void spec_slice_geom(SpecGeom* g) {
   const int Dt = g->D > 128 ? g->D - 128 : 0;
   if (g->NO > 64) return;
   g->slDt = Dt;
-  // GEMMs on the bf16 matrix cores through the exact three-term split with TR_SLICE_SPLIT=1
+  // GEMMs on the bf16 matrix cores through the exact three-term split unless TR_SLICE_SPLIT=0
   const char* spl = std::getenv("TR_SLICE_SPLIT");
-  g->slSp = (spl != nullptr && spl[0] == '1') ? (g->Rn <= 8 ? 1 : 2) : 0;
+  g->slSp = (spl != nullptr && spl[0] == '0') ? 0 : (g->Rn <= 8 ? 1 : 2);
   g->sl_Dp = ((g->D > 128 ? g->D : 128) + 3) & ~3;
   g->sl_oTail = SL_NW * SL_SLICE;
   g->sl_oEx = g->sl_oTail + SL_NW * SL_TAIL;
