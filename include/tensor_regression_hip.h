@@ -249,7 +249,11 @@ int tr_adam_step_f64(tr_plan* plan, double* params, const double* grad, double* 
  * the plan picks (tr_plan_describe):
  *   slice-1pass-mfma   training at n_w = 256, 97 <= n_d <= 130 (n_d >= 128 or n_d % 4 == 0),
  *                      1 <= Rn <= 16, Rs * n_complex <= 16 with n_complex in {1, 2, 4},
- *                      n_out <= 64 (and its LDS fits): column-slice single pass (config 5)
+ *                      n_out <= 64 (and its LDS fits): column-slice single pass (config 5);
+ *                      described as slice-1pass-mfma-bf16x3 when its GEMMs run on the bf16 matrix
+ *                      cores through an exact three-term split of the fp32 operands (the default;
+ *                      fp32 accumulation, same results as the f32 MFMA form to fp32 rounding;
+ *                      environment TR_SLICE_SPLIT=0 selects the f32 form)
  *   fused-1pass-mfma   K <= 32, n_w, n_d, n_out <= 256 and the whole sample + scratch in LDS:
  *                      single pass; also every tr_forward / tr_spectral_latents of such a plan
  *   generic-3kernel-mfma  any other shape in the envelope: T_n staged through HBM (three kernels)

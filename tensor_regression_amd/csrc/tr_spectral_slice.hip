@@ -224,6 +224,15 @@ __device__ __forceinline__ void sl_dma16(const float* gsrc, const float* lds_dst
                : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(sl_lds_addr(lds_dst)))
                : "memory");
 }
+// one 16-B LDS-DMA piece per lane through a buffer descriptor: rsrc base + soff + voff (lane) -> LDS
+// byte address m0 + 16 * lane; no per-lane 64-bit address arithmetic at the call
+__device__ __forceinline__ void sl_dma16b(__amdgpu_buffer_rsrc_t rs, uint32_t soff, uint32_t voff, const float* lds_dst) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds" SL_NT "\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(rs), "s"(__builtin_amdgcn_readfirstlane(sl_lds_addr(lds_dst))), "s"(soff)
+               : "memory");
+}
 // s_waitcnt vmcnt(n), n wave-uniform in [0, 63]
 __device__ __forceinline__ void sl_wait_vm(int n) {
 #define SL_VM(k) \
@@ -372,17 +381,30 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
   // memory pipeline as much as a dwordx4 one: ~3 vs ~6.8 TB/s chip-wide, tools/ldsdma_probe.hip.)
   // The per-lane offsets are recomputed from an opaque copy of the lane index at every call:
   // hoisted out of the sample loop they would hold 16 address registers.
-  auto dma_piece = [&](int64_t n, int q, int c4) {  // chunks 8q + 4c4 .. +3
-    int ln = lane;
-    asm volatile("" : "+v"(ln));
-    const int lsl = ln & 15, lc = ln >> 4;
-    const float* src = X + n * xld + (int64_t)(wbase + 16 * q) * D;
+  // The lane part of a piece's source is the same for every tile and sample: two byte offsets
+  // (c4 = 0, 1) held for the launch; the sample base goes into a buffer descriptor (SGPRs) and
+  // the tile's row offset into soffset, so a piece costs no per-lane address arithmetic.
+  uint32_t dvo[2];
+#pragma unroll
+  for (int c4 = 0; c4 < 2; ++c4) {
+    const int lsl = lane & 15, lc = lane >> 4;
     const int x = 4 * c4 + lc;  // chunk within the tile (= r & 7)
     const int sp = lsl ^ sl_swz(x);
     int d = dbase + 4 * (sp & 7);
     d = d < D ? d : 0;  // a column quad past D (D < 128, D % 4 == 0): any valid quad, times zero
-    sl_dma16(src + ((2 * x + (sp >> 3)) * D + d), slice + 64 * (8 * q + 4 * c4));
+    dvo[c4] = (uint32_t)(((2 * x + (sp >> 3)) * D + d) * 4);
+  }
+  const uint32_t sbytes = (uint32_t)(g.W * D * 4);
+  auto rsrc_of = [&](int64_t n) {
+    const uint64_t a = (uint64_t)(uintptr_t)(X + n * xld);
+    const uint64_t au = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(a >> 32)) << 32) |
+                        (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)au, (short)0, (int)sbytes, 0x00020000);
   };
+  auto dma_piece_r = [&](__amdgpu_buffer_rsrc_t rs, int q, int c4) {  // chunks 8q + 4c4 .. +3
+    sl_dma16b(rs, (uint32_t)((wbase + 16 * q) * D * 4), dvo[c4], slice + 64 * (8 * q + 4 * c4));
+  };
+  auto dma_piece = [&](int64_t n, int q, int c4) { dma_piece_r(rsrc_of(n), q, c4); };
   auto dma_tile = [&](int64_t n, int q) {
     dma_piece(n, q, 0);
     dma_piece(n, q, 1);
