@@ -46,7 +46,7 @@
                          // 2 no forward MFMAs, 4 no gradient MFMAs
 #endif
 #ifndef TR_SLICE_PRIO
-#define TR_SLICE_PRIO 1  // s_setprio 1 for the second-dispatched half (waves 4-7)
+#define TR_SLICE_PRIO 1  // s_setprio 1 for the second-dispatched half (waves 4-7); 2: for the first half
 #endif
 #ifndef TR_SLICE_BPF
 #define TR_SLICE_BPF 1  // gradient GEMM: next tile's operand reads issued before this tile's MFMAs
@@ -68,6 +68,10 @@
 #endif
 #ifndef TR_SLICE_PFAT
 #define TR_SLICE_PFAT 0  // 0: prefetch at the top of the sample (before the forward), 1: after the forward
+#endif
+#ifndef TR_SLICE_BKW
+#define TR_SLICE_BKW 4  // wave that keeps the per-sample bookkeeping (dA2 / dC2 / bias / loss / y_hat,
+                        // tail-row sums): a second-half wave, off the first half's critical path
 #endif
 #ifndef TR_SLICE_PROFILE
 #define TR_SLICE_PROFILE 0  // profiling build: per-phase cycle counts of wave 0 of workgroups 0..255
@@ -293,8 +297,8 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
   float* sB = sCC + NO * 16;                        // [NO] bias
   float* sWt = sB + NO;                             // [16] w_r
   float* sAcc = sWt + 16;                           // [NO*Rn] dA2 | [NO*Rs] dC2 | [NO] dbias
-  float* sTacc = sAcc + NO * (Rn + Rs + 1);         // wave 0: [Dt][dPhi(A1) 16 | dPhi(C1) 16] of rows 128+
-  double* sLoss = reinterpret_cast<double*>(lds + g.sl_oLoss);  // wave 0 lane 0: sum of squared errors
+  float* sTacc = sAcc + NO * (Rn + Rs + 1);         // bookkeeping wave: [Dt][dPhi(A1) 16 | dPhi(C1) 16] of rows 128+
+  double* sLoss = reinterpret_cast<double*>(lds + g.sl_oLoss);  // bookkeeping wave lane 0: sum of squared errors
 
   for (int e = g.sl_oTail + t; e < g.sl_lds_floats; e += SL_T) lds[e] = 0.f;
   __syncthreads();
@@ -445,7 +449,8 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
     }
   };
   if (nr > 0) dma_sample(sample_of(0));
-  if (TR_SLICE_PRIO && hw == 1) __builtin_amdgcn_s_setprio(1);
+  if (TR_SLICE_PRIO == 1 && hw == 1) __builtin_amdgcn_s_setprio(1);
+  if (TR_SLICE_PRIO == 2 && hw == 0) __builtin_amdgcn_s_setprio(1);
 #if TR_SLICE_PROFILE
   unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long prof_t = __builtin_readcyclecounter();
@@ -535,6 +540,10 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
       }
     }
     if (TR_SLICE_PFAT && NPF > 0 && has_next) prefetch(nn);
+    // y of the first two outputs by scalar loads issued here: their latency hides under the
+    // exchange, barrier A and the column partials (issued inside the output loop it was exposed;
+    // issued before the forward, an SMEM load in flight turns its counted LDS waits into lgkmcnt(0))
+    const float y0 = y[n * NO], y1 = NO > 1 ? y[n * NO + 1] : 0.f;
     // lane-dependent indices of the epilogue from an opaque copy of the lane index: every LDS
     // address below is then formed here (a few VALU ops) instead of living across the loop
     // (held through the GEMMs, the split kernels spilled them to scratch: a vmcnt(0) reload each)
@@ -661,7 +670,7 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
     const float c1t = (Dt > 0 && gq < Dt && rs_ok) ? sC1[rs * Dp + dtl] : 0.f;
     zp = sl_groups_sum(zp);
     vp = sl_groups_sum(vp);
-    if (wv == 0 && Dt > 0) {  // wave 0 adds the tail rows' terms
+    if (wv == TR_SLICE_BKW && Dt > 0) {  // the bookkeeping wave adds the tail rows' terms
       float zt = n1t * tt1;
       float vt = vlane ? c1t * Mt : 0.f;
       zp += sl_groups_sum(zt);
@@ -694,11 +703,11 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
       const float b = sB[o];
       const float yh = (Rn > 0 ? pl + b : 0.f) + (Rs > 0 ? ps + b : 0.f);
       // y by a scalar load (a vector load's compiler-inserted vmcnt(0) would drain the prefetch)
-      const float e = yh - y[n * NO + o];
+      const float e = yh - (o == 0 ? y0 : (o == 1 ? y1 : y[n * NO + o]));
       const float rv = e * scale;
       dz = fmaf(rv, ca, dz);
       dv = fmaf(rv, sCC[o * 16 + rs], dv);
-      if (wv == 0 && lk < 16) {
+      if (wv == TR_SLICE_BKW && lk < 16) {
         if (i < Rn) sAcc[o * Rn + i] += sWt[i] * rv * zi;
         if (i < Rs) sAcc[NO * Rn + o * Rs + i] += rv * vi;
         if (lk == 0) {
@@ -730,7 +739,7 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
     if (Dt > 0) {
       dTt1 = dz * n1t;
       dTt0 = Mt > 0.f ? dv * c1t * __builtin_amdgcn_rcpf(Mt) * tt0 : 0.f;
-      if (wv == 0 && gq < Dt) {
+      if (wv == TR_SLICE_BKW && gq < Dt) {
         if (i < Rn) sTacc[gq * 32 + i] = fmaf(dz, tt1, sTacc[gq * 32 + i]);
         if (vlane) sTacc[gq * 32 + 16 + rs] = fmaf(dv, Mt, sTacc[gq * 32 + 16 + rs]);
       }
@@ -928,8 +937,8 @@ void spec_slice_geom(SpecGeom* g) {
   const int64_t small = (int64_t)g->sl_Dp * (g->Rn + g->Rs) + (int64_t)g->NO * 33 + 16 +
                         (int64_t)g->NO * (g->Rn + g->Rs + 1) + 2 * 32;
   g->sl_oLoss = (int)(g->sl_oN1 + ((small + 3) & ~(int64_t)3));  // 16-B aligned double
-  g->sl_oPF = g->sl_oLoss + 4;  // 64 floats: landing line of the L2 prefetch (never read)
-  const int64_t tot = g->sl_oPF + 64;
+  g->sl_oPF = g->sl_oLoss + 4;  // 64 floats (with TR_SLICE_PF): landing line of the L2 prefetch (never read)
+  const int64_t tot = g->sl_oPF + (TR_SLICE_PF > 0 ? 64 : 0);
   if (tot * 4 > 160 * 1024) return;
   g->sl_lds_floats = (int)tot;
   g->sl = 1;
