@@ -158,9 +158,26 @@ __device__ __forceinline__ void sl_split_m(float a, float b, sl_u4 (&f)[3], int 
   f[1][m] = h2;
   f[2][m] = h3;
 }
+#ifndef TR_SLICE_X2
+#define TR_SLICE_X2 0  // experiment build only: the X side (first operand at every call site) as
+                       // two round-to-nearest bf16 pieces (NOT exact: representation error up to
+                       // 2^-16 |x|, median 2^-19.4): five / three MFMAs per product
+#endif
+// X-side split: three exact pieces, or with TR_SLICE_X2 two round-to-nearest ones (x3 unused)
+__device__ __forceinline__ void sl_splitx_m(float a, float b, sl_u4 (&f)[3], int m) {
+#if TR_SLICE_X2
+  typedef __bf16 sl_bf2 __attribute__((ext_vector_type(2)));
+  const uint32_t h1 = __builtin_bit_cast(uint32_t, sl_bf2{(__bf16)a, (__bf16)b});
+  const float ra = a - __uint_as_float(h1 << 16), rb = b - __uint_as_float(h1 & 0xffff0000u);
+  f[0][m] = h1;
+  f[1][m] = __builtin_bit_cast(uint32_t, sl_bf2{(__bf16)ra, (__bf16)rb});
+#else
+  sl_split_m(a, b, f, m);
+#endif
+}
 // c += A.B over the six cross terms (A, B each as three split fragments)
 __device__ __forceinline__ sl_f4 sl_mfma6(const sl_u4 (&a)[3], const sl_u4 (&b)[3], sl_f4 c) {
-  c = sl_mfma_bf(a[2], b[0], c);
+  if (!TR_SLICE_X2) c = sl_mfma_bf(a[2], b[0], c);
   c = sl_mfma_bf(a[1], b[1], c);
   c = sl_mfma_bf(a[0], b[2], c);
   c = sl_mfma_bf(a[1], b[0], c);
@@ -172,7 +189,7 @@ __device__ __forceinline__ sl_f4 sl_mfma6(const sl_u4 (&a)[3], const sl_u4 (&b)[
 // product is the sum of accumulator columns c and c + 8 (folded by sl_fold8): four MFMAs for
 // the six cross terms (a3b2 comes along)
 __device__ __forceinline__ sl_f4 sl_mfma_lp(const sl_u4 (&a)[3], const sl_u4 (&b)[2], sl_f4 c) {
-  c = sl_mfma_bf(a[2], b[0], c);
+  if (!TR_SLICE_X2) c = sl_mfma_bf(a[2], b[0], c);
   c = sl_mfma_bf(a[0], b[1], c);
   c = sl_mfma_bf(a[1], b[0], c);
   c = sl_mfma_bf(a[0], b[0], c);
@@ -505,8 +522,8 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
           // tile q holds elements 4 (q & 1) .. +3 of k step q / 2: VGPRs 2 (q & 1), 2 (q & 1) + 1
 #pragma unroll
           for (int mm = 0; mm < 2; ++mm) {
-            sl_split_m(xa[2 * mm].x, xa[2 * mm + 1].x, xf[0], 2 * (q & 1) + mm);
-            sl_split_m(xa[2 * mm].y, xa[2 * mm + 1].y, xf[1], 2 * (q & 1) + mm);
+            sl_splitx_m(xa[2 * mm].x, xa[2 * mm + 1].x, xf[0], 2 * (q & 1) + mm);
+            sl_splitx_m(xa[2 * mm].y, xa[2 * mm + 1].y, xf[1], 2 * (q & 1) + mm);
           }
           if ((q & 1) && !(TR_SLICE_SKIP & 2)) {
             const int S = q >> 1;
@@ -570,7 +587,7 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
         for (int m = 0; m < 4; ++m) {
           const float x0 = i < Dt ? sTail[i * TR + 8 * m + gq] : 0.f;
           const float x1 = i < Dt ? sTail[i * TR + 8 * m + 4 + gq] : 0.f;
-          sl_split_m(x0, x1, tf, m);
+          sl_splitx_m(x0, x1, tf, m);
         }
         auto tail_step = [&](const sl_u4(&b_s)[3], const sl_u4(&b_l)[NL]) {
           Tts = sl_mfma6(tf, b_s, Tts);
@@ -821,7 +838,7 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
 #pragma unroll
             for (int v = 0; v < 4; ++v) {
               const sl_f4& src = v < 2 ? va : vb;
-              sl_split_m(src[2 * (v & 1) + 0], src[2 * (v & 1) + 1], af, v);
+              sl_splitx_m(src[2 * (v & 1) + 0], src[2 * (v & 1) + 1], af, v);
             }
             if (has_next) {
               asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // tile q's reads landed
