@@ -4,6 +4,12 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4] [--no-cpu-baseline]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N ...   (N > 1)
 
+`--gpus N` outside a launcher (no WORLD_SIZE in the environment) starts the N ranks itself: one
+child process per GPU with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT
+set as torchrun sets them, so the N > 1 path is the one torchrun runs; the parent never touches
+the GPU, passes rank 0's JSON line through and exits non-zero (no JSON line) if any rank fails
+or fewer than N devices are visible.  Under a launcher, WORLD_SIZE must equal --gpus.
+
 A "step" is one fit_Adam iteration of the reference (standard_tensor_regression.py:458-470):
 forward + MSE (+L2) + gradient + Adam over every sample the rank holds.  Default workload =
 BASELINE.json configs[1]: X (65536, 256, 128) fp32 per GPU, rank 8 (weak scaling: every rank
@@ -241,13 +247,56 @@ def host_stream_report(model, hs, Xres, y, fit, ms_step, dev):
             "overlap_hidden_frac": overlap, "chunk_rows": hs.chunk_rows, "bytes_per_step": nbytes}
 
 
+def launch_ranks(n, argv, json_out):
+    """Start the N ranks of `bench.py --gpus N` as child processes (torchrun's environment; the
+    parent makes no HIP call: torch.cuda.device_count() does not initialise HIP on this image).
+    Returns the exit code; rank 0's stdout (the JSON line) is written only if every rank succeeded."""
+    import socket
+    import subprocess
+    visible = torch.cuda.device_count()
+    if visible < n:
+        log(f"bench: --gpus {n} needs {n} visible GPUs, found {visible}; no measurement")
+        return 2
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    pending = set(range(n))
+    while pending:
+        for r in sorted(pending):
+            code = procs[r].poll()
+            if code is None:
+                continue
+            pending.discard(r)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                log(f"bench: rank {r} exited with {code}; stopping the other ranks")
+                for q in pending:
+                    procs[q].terminate()
+        time.sleep(0.05)
+    out = procs[0].stdout.read().decode()
+    if rc == 0:
+        json_out.write(out)
+        json_out.flush()
+    return rc
+
+
 def main():
     # exactly ONE line on stdout: route everything else (RCCL's banner, library prints) to stderr
     json_out = os.fdopen(os.dup(1), "w")
     sys.stdout.flush()
     os.dup2(2, 1)
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks) of the run: under a launcher WORLD_SIZE must match; without one, N > 1 "
+                         "starts the N ranks as child processes (default: WORLD_SIZE or 1)")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=None,
                     help="untimed fit_Adam iterations first: the compute-bound kernels (c3, c5) reach their "
@@ -267,6 +316,16 @@ def main():
     ap.add_argument("--traffic", default=os.path.join(HERE, "profiles", "traffic.json"),
                     help="PMC traffic summary (tools/pmc_traffic.py output) for the roofline 'traffic' field")
     args = ap.parse_args()
+    env_world = os.environ.get("WORLD_SIZE")
+    if args.gpus is None:
+        args.gpus = int(env_world) if env_world else 1
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:], json_out))
+    if env_world is not None and int(env_world) != args.gpus:
+        log(f"bench: --gpus {args.gpus} but the launcher started WORLD_SIZE={env_world} ranks; no measurement")
+        sys.exit(2)
     cfg = CONFIGS[args.config]
     if args.warmup is None:  # 200 (< 0.5 s) resident; the PCIe-bound streamed config: 3 (0.5 s)
         args.warmup = cfg.get("default_warmup", 200)

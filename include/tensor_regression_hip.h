@@ -252,7 +252,9 @@ int tr_adam_step_f64(tr_plan* plan, double* params, const double* grad, double* 
  *                      n_out <= 64 (and its LDS fits): column-slice single pass (config 5);
  *                      described as slice-1pass-mfma-bf16x3 when its GEMMs run on the bf16 matrix
  *                      cores through an exact three-term split of the fp32 operands (the default;
- *                      fp32 accumulation, same results as the f32 MFMA form to fp32 rounding;
+ *                      fp32 accumulation; each product a.b is formed to < 2^-20 |ab| in the worst
+ *                      case, typically 2^-25, against the f32 form's rounding of 2^-24, so results
+ *                      are not bitwise those of the f32 MFMA form;
  *                      environment TR_SLICE_SPLIT=0 selects the f32 form)
  *   fused-1pass-mfma   K <= 32, n_w, n_d, n_out <= 256 and the whole sample + scratch in LDS:
  *                      single pass; also every tr_forward / tr_spectral_latents of such a plan

@@ -559,6 +559,9 @@ def fit_state(plan, dtype, amsgrad):
 
 # ---- the per-iteration gradient all-reduce -------------------------------------------------------
 _RCCL_DIRECT = os.environ.get("TR_RCCL_DIRECT", "1") != "0"
+# seconds a host sync of a sharded fit waits for the direct all-reduce before aborting the
+# communicator (a dead or diverged peer would otherwise block the survivors forever)
+_RCCL_TIMEOUT = float(os.environ.get("TR_RCCL_TIMEOUT", "600"))
 _rccl_comms = {}
 
 
@@ -590,7 +593,10 @@ def _rccl_lib():
     lib.ncclCommDestroy.argtypes = [ctypes.c_void_p]
     lib.ncclGetErrorString.restype = ctypes.c_char_p
     lib.ncclGetErrorString.argtypes = [ctypes.c_int]
-    for fn in ("ncclGetUniqueId", "ncclCommInitRank", "ncclAllReduce", "ncclCommDestroy"):
+    lib.ncclCommGetAsyncError.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
+    lib.ncclCommAbort.argtypes = [ctypes.c_void_p]
+    for fn in ("ncclGetUniqueId", "ncclCommInitRank", "ncclAllReduce", "ncclCommDestroy", "ncclCommGetAsyncError",
+               "ncclCommAbort"):
         getattr(lib, fn).restype = ctypes.c_int
     return lib
 
@@ -611,6 +617,7 @@ class RcclAllReduce:
         self.dev = int(device_index)
         ranks = dist.get_process_group_ranks(process_group)
         me = dist.get_rank(process_group)
+        self.size = len(ranks)
         uid = _UniqueId()
         if me == 0:
             self._check(self.lib.ncclGetUniqueId(ctypes.byref(uid)), "ncclGetUniqueId")
@@ -630,6 +637,40 @@ class RcclAllReduce:
         p = ctypes.c_void_p(t.data_ptr())
         self._check(self.lib.ncclAllReduce(p, p, t.numel(), dt, 0, self.comm, stream_handle(self.dev)),
                     "ncclAllReduce")
+
+    def wait(self, timeout=None):
+        """Block until the work queued on the current stream (this rank's all-reduces included) has
+        finished, polling the communicator: an asynchronous RCCL error or `timeout` seconds
+        (TR_RCCL_TIMEOUT, default 600) without progress aborts the communicator and raises, so a
+        rank whose peer died does not hang in the next host sync.  ProcessGroupNCCL's watchdog does
+        this for torch's own collectives; this communicator is outside it."""
+        import time
+        timeout = _RCCL_TIMEOUT if timeout is None else timeout
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.dev))
+        t0 = time.monotonic()
+        spins = 0
+        while not ev.query():
+            err = ctypes.c_int(0)
+            rc = self.lib.ncclCommGetAsyncError(self.comm, ctypes.byref(err))
+            if rc != 0 or err.value not in (0, 7):  # 7 = ncclInProgress
+                self.abort()
+                raise RuntimeError(f"RCCL all-reduce of the sharded fit failed asynchronously: "
+                                   f"{self.lib.ncclGetErrorString(err.value or rc).decode()}")
+            if time.monotonic() - t0 > timeout:
+                self.abort()
+                raise RuntimeError(f"RCCL all-reduce of the sharded fit made no progress for {timeout:.0f} s "
+                                   "(a peer rank died or left the fit); the communicator was aborted")
+            spins += 1
+            time.sleep(0 if spins < 2000 else 1e-4)
+
+    def abort(self):
+        if self.comm is not None and self.comm.value:
+            self.lib.ncclCommAbort(self.comm)
+            self.comm = None
+        for k, v in list(_rccl_comms.items()):
+            if v is self:
+                del _rccl_comms[k]
 
     def destroy(self):
         if self.comm is not None and self.comm.value:
@@ -727,6 +768,8 @@ def _adam_loop(plan, X, target, class_weight, norm, arena, weights, lambda_L2, m
                 allreduce(grad)
             plan.adam_step(arena, grad, m, v, vmax, lambda_L2, hp, it + 1, hist, base, it, patience, tol, stop)
         ii += n
+        if isinstance(allreduce, RcclAllReduce) and allreduce.size > 1:
+            allreduce.wait()  # the host sync below, with a watchdog on the peers
         stopped_at = int(stop.item())  # one host sync per chunk
         if stopped_at <= _lib.TR_STOP_DEVICE_ERROR:
             # a pass failed on the device (on any rank: the status slot is all-reduced with the

@@ -121,7 +121,9 @@ __device__ __forceinline__ sl_f4 sl_mfma(float a, float b, sl_f4 c) {
 // the (exact) remainder, x3 = the rest (at most 8 significant bits: exactly a bf16).  A product
 // a.b is formed as the six cross terms of weight >= 2^-16 (a1b1, a1b2, a2b1, a1b3, a2b2, a3b1)
 // on v_mfma_f32_16x16x32_bf16 (16x the f32 MFMA rate); the dropped terms a2b3, a3b2, a3b3
-// weigh <= 2^-24 |ab|, i.e. the f32 rounding of the product itself.
+// weigh < 2^-20 |ab| in the worst case (truncation bounds |x2| < 2^-7 |x|, |x3| < 2^-14 |x|;
+// measured maximum 2^-21.3) and typically 2^-25, below the f32 rounding of the product (2^-24);
+// tests/test_split_numerics.py holds both bounds.
 typedef __bf16 sl_bf8 __attribute__((ext_vector_type(8)));
 typedef uint32_t sl_u4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ sl_f4 sl_mfma_bf(sl_u4 a, sl_u4 b, sl_f4 c) {

@@ -143,5 +143,9 @@ class HostStream:
                 issue(c + 1)
             b = c % 2
             compute.wait_event(self.copied[b])
-            yield r0, r1, self.bufs[b][: r1 - r0]
-            self.consumed[b].record(compute)
+            try:
+                yield r0, r1, self.bufs[b][: r1 - r0]
+            finally:
+                # also when the consumer raises or abandons the pass: the kernels it already
+                # queued on this buffer must finish before a later pass copies into it
+                self.consumed[b].record(compute)

@@ -31,7 +31,7 @@ def load(name):
     meta = json.loads(str(d.pop("meta")))
     shapes = [tuple(s) for s in meta["factor_shapes"]]
     dt = np.float64 if meta.get("model") == "linear_f64" else np.float32
-    d["X"] = torch.tensor(d["X_q"].astype(dt) / 8.0)
+    d["X"] = _x_of(d, dt)
     d["Bcp0_list"] = split(d["Bcp0"], shapes, dt)
     if "Bcp_final" in d:
         d["Bcp_final_list"] = split(d["Bcp_final"], shapes, dt)
@@ -44,6 +44,14 @@ def load(name):
     d["meta"] = meta
     d["shapes"] = shapes
     return d
+
+
+def _x_of(d, dt):
+    """X of a fixture: int8 / 8 (exact in fp32 and in bf16), or stored as float32 (X_f32:
+    full-mantissa inputs, the *_f32x fixtures)."""
+    if "X_f32" in d:
+        return torch.tensor(d["X_f32"].astype(dt))
+    return torch.tensor(d["X_q"].astype(dt) / 8.0)
 
 
 def normwise_rel(a, b):
@@ -59,7 +67,7 @@ def load_spectral(name):
     meta = json.loads(str(d.pop("meta")))
     sn = [tuple(s) for s in meta["factor_shapes_n"]]
     sc = [tuple(s) for s in meta["factor_shapes_c"]]
-    d["X"] = torch.tensor(d["X_q"].astype(np.float32) / 8.0)
+    d["X"] = _x_of(d, np.float32)
     for key in ("Bcp_n0", "Bcp_n_10", "Bcp_n_final", "grads_n0"):
         if key in d:
             d[key + "_list"] = split(d[key], sn) if d[key].size else [np.zeros(s, np.float32) for s in sn]

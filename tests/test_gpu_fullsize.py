@@ -205,3 +205,92 @@ def test_spectral_full_size_properties():
     lr = model.loss_running
     assert len(lr) == 3 and all(np.isfinite(lr)), lr
     assert abs(lr[0] - loss.item()) <= 1e-6 * abs(loss.item()), (lr[0], loss.item())
+
+
+def _spectral_fp64(X, y, Bn, Bc, bias, lam):
+    """fp64 closed form of the spectral fit loss and gradients (cp_oracle.closed_form_spectral,
+    restated in torch on the device and chunked over samples; spectral_tensor_regression.py
+    lin_model :118-165 + stepwise_spectral_model :339-390, loss :716-717; no softplus, unit
+    weights, bias added by both terms)."""
+    N, W, D = X.shape
+    O = y.shape[1]
+    A = [a.detach().double()[:, :, 0] for a in Bn]
+    C = [c.detach().double() for c in Bc]
+    Rn, Rs, Cc = A[0].shape[1], C[0].shape[1], C[0].shape[2]
+    b = bias.detach().double()
+    Phi0 = torch.cat([A[0], C[0].reshape(W, Rs * Cc)], dim=1)
+    C1, C2 = C[1][:, :, 0], C[2][:, :, 0]
+    sse = torch.zeros((), dtype=torch.float64, device=DEV)
+    gA = [torch.zeros_like(a) for a in A]
+    gC = [torch.zeros_like(c) for c in C]
+    dPhi0 = torch.zeros_like(Phi0)
+    gb = torch.zeros_like(b)
+    ch = CHUNK // 2
+    for a in range(0, N, ch):
+        Xc = X[a:a + ch].double()
+        n = Xc.shape[0]
+        T = torch.einsum('nwd,wk->ndk', Xc, Phi0)
+        Z = torch.einsum('ndr,dr->nr', T[:, :, :Rn], A[1])
+        Tc = T[:, :, Rn:].reshape(n, D, Rs, Cc)
+        M = torch.sqrt((Tc * Tc).sum(3))
+        V = torch.einsum('ndr,dr->nr', M, C1)
+        yhat = Z @ A[2].T + b + V @ C2.T + b
+        res = yhat - y[a:a + ch].double()
+        sse += (res * res).sum()
+        r = 2.0 * res / (N * O)
+        gb += 2.0 * r.sum(0)
+        gA[2] += r.T @ Z
+        dZ = r @ A[2]
+        gA[1] += torch.einsum('nr,ndr->dr', dZ, T[:, :, :Rn])
+        gC[2] += (r.T @ V)[:, :, None]
+        dV = r @ C2
+        gC[1] += torch.einsum('nr,ndr->dr', dV, M)[:, :, None]
+        dM = dV[:, None, :] * C1[None]
+        q = torch.where(M > 0, dM / torch.where(M > 0, M, torch.ones_like(M)), torch.zeros_like(M))
+        dT = torch.cat([dZ[:, None, :] * A[1][None], (q[..., None] * Tc).reshape(n, D, Rs * Cc)], dim=2)
+        dPhi0 += torch.einsum('nwd,ndk->wk', Xc, dT)
+        del Xc, T, Tc, dT
+    gA[0] = dPhi0[:, :Rn]
+    gC[0] = dPhi0[:, Rn:].reshape(W, Rs, Cc)
+    grads = [g[:, :, None] for g in gA] + gC
+    pen = 0.0
+    for i, p in enumerate([a.detach().double() for a in list(Bn) + list(Bc)]):
+        nrm = torch.linalg.norm(p)
+        pen += float(nrm)
+        grads[i] = grads[i] + lam * p / nrm
+    data = float(sse) / (N * O)
+    return data, data + lam * pen, grads, gb
+
+
+def test_spectral_full_size_vs_fp64():
+    """Config 5 at full size (X (32768, 256, 129), rank_normal = rank_spectral = 8, n_complex_dim 1,
+    y (N, 2)) on the product kernel (k_spec_slice, exact bf16x3 split GEMMs) against the fp64
+    closed form: the same bar as configs 2-4."""
+    from tensor_regression_amd.spectral_tensor_regression import CP_linear_regression
+    N, W, D, O = 32768, 256, 129, 2
+    gen = torch.Generator(device=DEV).manual_seed(1234)
+    X = torch.randn((N, W, D), device=DEV, generator=gen).abs_()
+    y = torch.randn((N, O), device=DEV, generator=gen)
+    torch.manual_seed(1)
+    model = CP_linear_regression(X.shape, y.shape, rank_normal=8, rank_spectral=8, n_complex_dim=1, device=DEV)
+    plan = model._get_plan(X, N)
+    assert "slice-1pass-mfma-bf16x3" in plan.describe and "slsp=1" in plan.describe, plan.describe
+    arena = plan.pack(model.Bcp_n, model.Bcp_c, model.bias)
+    w = torch.ones(16, device=DEV)
+    lam = 0.01
+    grad = torch.zeros(plan.num_grads, device=DEV)
+    gtot = torch.zeros(plan.num_params, device=DEV)
+    loss = torch.zeros(1, device=DEV)
+    plan.loss_grad(X, y, None, float(N * O), arena, w, grad)
+    plan.finalize_grad(arena, grad, lam, gtot, loss)
+    data, total, grads, gb = _spectral_fp64(X, y, model.Bcp_n, model.Bcp_c, model.bias, lam)
+    errs = {"data_loss": abs(grad[plan.num_params].item() - data) / abs(data),
+            "loss": abs(loss.item() - total) / abs(total),
+            "bias": normwise_rel(gtot[plan.offsets[6]:].cpu().numpy(), gb.cpu().numpy())}
+    for f, (v, ref) in enumerate(zip(plan.factor_views(gtot), grads)):
+        errs[f"grad{f}"] = normwise_rel(v.cpu().numpy(), ref.cpu().numpy())
+    print("c5", plan.describe, errs)
+    assert errs["data_loss"] <= LOSS_TOL and errs["loss"] <= LOSS_TOL, errs
+    for f in range(6):
+        assert errs[f"grad{f}"] <= GRAD_TOL, errs
+    assert errs["bias"] <= 1e-5, errs

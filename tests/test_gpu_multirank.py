@@ -12,7 +12,12 @@ and the gfx950 kernels.  Each rank fits its own sample shard:
   * linear, single-pass fused path          (k_linear_fused)
   * linear, wide rows                       (k_linear_cluster; two processes share the GPU, so
                                              its exchange may time out and the fit resume on the
-                                             two-pass path — on BOTH ranks, at the same iteration)
+                                             two-pass path — on BOTH ranks, at the same iteration;
+                                             which path each rank ran is printed)
+  * linear, wide rows, ranks in turns       (k_linear_cluster with each rank's gradient pass run
+                                             while the other rank's queue is drained and parked at
+                                             a barrier: the kernels never share the GPU in time, so
+                                             the single pass must complete on both ranks)
   * multinomial, config-3 sample shape      (k_mnl_duo), model built WITHOUT Bcp_init: rank 1's
                                              shard misses the top class and a middle class and
                                              starts from another seed
@@ -36,7 +41,7 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
 RTOL = 1e-5
 ITERS = 20
-CASES = ("linear_fused", "linear_cluster", "mnl_duo", "spectral_slice")
+CASES = ("linear_fused", "linear_cluster", "linear_cluster_turns", "mnl_duo", "spectral_slice")
 
 
 def _data(case):
@@ -48,7 +53,7 @@ def _data(case):
         y = torch.randn(3000, generator=g)
         init = [torch.randn(d, 6, generator=g) * 0.3 for d in (64, 32)]
         return X, y, 1300, init
-    if case == "linear_cluster":
+    if case.startswith("linear_cluster"):
         X = torch.randn(600, 64, 64, 32, generator=g)
         y = torch.randn(600, generator=g)
         init = [torch.randn(d, 16, generator=g) * 0.3 for d in (64, 64, 32)]
@@ -99,18 +104,41 @@ def _fit(case, X, y, init, seed, process_group=None):
     return list(m.loss_running), facs, m._plan.describe
 
 
+def _in_turns(fn, rank, world):
+    """fn (a rank's gradient pass) run while every other rank's GPU queue is drained and the rank
+    is parked at a barrier: the ranks' kernels never overlap in time."""
+    import torch.distributed as dist
+
+    def wrapped(*a, **k):
+        torch.cuda.synchronize()
+        for r in range(world):
+            dist.barrier()
+            if r == rank:
+                fn(*a, **k)
+                torch.cuda.synchronize()
+        dist.barrier()
+    return wrapped
+
+
 def _worker(rank, world, port, out):
     import torch.distributed as dist
+    from tensor_regression_amd import _engine
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     res = {}
     for case in CASES:
         X, y, split, init = _data(case)
         lo, hi = (0, split) if rank == 0 else (split, X.shape[0])
+        orig = _engine.loss_grad_any
+        if case.endswith("_turns"):
+            _engine.loss_grad_any = _in_turns(orig, rank, world)
         with warnings.catch_warnings(record=True) as w:
             warnings.simplefilter("always")
-            lr, facs, desc = _fit(case, X[lo:hi].contiguous(), y[lo:hi].contiguous(), init, seed=7 + 5 * rank,
-                                  process_group=dist.group.WORLD)
+            try:
+                lr, facs, desc = _fit(case, X[lo:hi].contiguous(), y[lo:hi].contiguous(), init, seed=7 + 5 * rank,
+                                      process_group=dist.group.WORLD)
+            finally:
+                _engine.loss_grad_any = orig
         res[case] = {"loss_running": lr, "factors": [torch.from_numpy(np.ascontiguousarray(f)) for f in facs],
                      "describe": desc, "warnings": [str(x.message) for x in w]}
     torch.save(res, f"{out}.{rank}")
@@ -136,19 +164,26 @@ def _single(case):
 
 
 @pytest.mark.parametrize("case", CASES)
-def test_world2_fit_matches_single_process(world2, case):
+def test_world2_fit_matches_single_process(world2, case, capsys):
     r0, r1 = world2[0][case], world2[1][case]
+    paths = [("recovered on the two-pass path" if "recovered=2pass" in r["describe"] else "single pass completed")
+             for r in (r0, r1)]
+    with capsys.disabled():
+        print(f"\n[world2 {case}] rank 0: {paths[0]}; rank 1: {paths[1]} ({r0['describe'].split(' path=')[1].split()[0]})")
     # the replicas are in lock-step: bitwise identical on both ranks
     assert r0["loss_running"] == r1["loss_running"]
     for a, b in zip(r0["factors"], r1["factors"]):
         assert torch.equal(a, b)
     # the kernel the case is about ran (the cluster pass may have recovered on the two-pass path:
     # two processes share the GPU, which is exactly what its status slot exists for)
-    want = {"linear_fused": "fused-1pass", "linear_cluster": "cluster-1pass", "mnl_duo": " duo ",
-            "spectral_slice": "slice-1pass"}[case]
+    want = {"linear_fused": "fused-1pass", "linear_cluster": "cluster-1pass", "linear_cluster_turns": "cluster-1pass",
+            "mnl_duo": " duo ", "spectral_slice": "slice-1pass"}[case]
     assert want in r0["describe"] and want in r1["describe"], (r0["describe"], r1["describe"])
     assert ("recovered=2pass" in r0["describe"]) == ("recovered=2pass" in r1["describe"])
     if case != "linear_cluster":
+        # with the ranks' passes apart in time the cluster exchange has no co-tenant: it must
+        # complete (no recovery, no warning) on both ranks
+        assert "recovered=2pass" not in r0["describe"], r0["describe"]
         assert not r0["warnings"] and not r1["warnings"], (r0["warnings"], r1["warnings"])
     # and equal to one process fitting the concatenated shards from the same initial point
     lr, facs, _ = _single(case)

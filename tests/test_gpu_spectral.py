@@ -123,6 +123,8 @@ def _spectral_golden(name, kind):
         assert ("slice-1pass" in desc) == (kind in ("fused", "slicef32")), desc
         # the default form runs its GEMMs through the exact bf16x3 split
         assert ("bf16x3" in desc) == (kind == "fused"), desc
+        if kind == "fused":  # lin columns packed (Rn <= 8) or unpacked (spec_slice_rn12_f32x)
+            assert f"slsp={1 if m['rank_normal'] <= 8 else 2}" in desc, desc
     # predict() = lin_model + spectral_model (spectral…py:959-960)
     _close(model.predict(X).numpy(), d["predict0"])
     # one forward + loss + gradient (fit model, spectral…py:716-720)
@@ -189,7 +191,10 @@ def _spectral_golden(name, kind):
                                          m["softplus_kwargs"]).numpy()
     assert normwise_rel(ref_fin, d["predict_final"]) <= RTOL  # the oracle's predict model is the reference's
     e_ref = normwise_rel(p_fin, d["predict_final"])
+    # hard bar whatever arm passes: the pre-round-3 fixed 1e-4 against the reference's output
+    assert e_ref <= 1e-4, e_ref
     if e_ref > RTOL:  # as accurate as the reference's own fp32 run, against the fp64 trajectory
+        print(f"predict_final: {e_ref:.2e} from the reference's output > {RTOL:g}; fp64-distance arm")
         r64p = cp_oracle.spectral_predict(X.cpu().double(), [torch.tensor(a).double() for a in r64["Bcp_n"]],
                                           [torch.tensor(a).double() for a in r64["Bcp_c"]],
                                           torch.ones(m["rank_normal"] + m["rank_spectral"], dtype=torch.float64),
@@ -242,6 +247,10 @@ SLICE_SHAPES = [
     (120, 256, 100, 5, 3, 5, 1, [False, False, False]),   # D < 128 (columns past D masked)
     (64, 256, 129, 8, 8, 8, 1, [False, False, False]),    # n_out = 8
     (64, 256, 129, 40, 8, 8, 1, [False, False, False]),   # n_out = 40: beyond the slice kernel's LDS
+    # 9 <= Rn <= 16: the split form with unpacked lin columns (SP = 2), every tail-row variant
+    (96, 256, 129, 2, 12, 4, 1, [False, False, False]),   # Rn = 12, one tail row
+    (80, 256, 100, 3, 16, 4, 1, [False, True, False]),    # Rn = 16, D < 128 (with D >= 129 beyond LDS)
+    (64, 256, 130, 2, 9, 2, 3, [True, False, False]),     # Rn = 9, Cc = 4, two tail rows
 ]
 # beyond the fused kernel's envelope: the generic path whatever TR_SPEC_GENERIC says
 WIDE_SHAPES = [
@@ -301,6 +310,8 @@ def _spectral_shape(N, W, D, O, Rn, Rs, ncd, nn, kind):
     slice_ok = _slice_shape(W, D, Rn, Rs, ncd, O)
     assert ("slice" in plan.describe) == (kind in ("fused", "slicef32") and slice_ok), plan.describe
     assert ("bf16x3" in plan.describe) == (kind == "fused" and slice_ok), plan.describe
+    if kind == "fused" and slice_ok:  # lin columns packed two split parts per tile (Rn <= 8) or not
+        assert f"slsp={1 if Rn <= 8 else 2}" in plan.describe, plan.describe
     arena = plan.pack(model.Bcp_n, model.Bcp_c, model.bias)
     w = torch.ones(Rn + Rs, device=DEV)
     grad = torch.zeros(plan.num_grads, device=DEV)

@@ -51,8 +51,10 @@ def test_six_term_product_error():
     exact = a.astype(np.float64) * b.astype(np.float64)
     nz = exact != 0
     rel = np.abs(six[nz] - exact[nz]) / np.abs(exact[nz])
-    assert rel.max() < 2.0 ** -20          # worst case of the dropped terms
-    assert np.median(rel) < 2.0 ** -24     # typically below the fp32 rounding of the product
+    # the bound the kernel comment, the public header and DESIGN.md state: < 2^-20 |ab| worst case
+    # (measured 2^-21.3 on this kind of sample), typically 2^-25 (below the fp32 product rounding)
+    assert rel.max() < 2.0 ** -20
+    assert np.median(rel) < 2.0 ** -24
 
 
 def test_packed_lin_columns_sum_to_the_six_terms():
