@@ -523,10 +523,13 @@ def main():
                                "algorithmic_bytes_per_launch": bytes_launch, "hbm_GBps": achieved,
                                "hbm_frac": achieved / HBM_PEAK_GBPS, "roofline_ms": 1e3 * t_mfma}
         out["dtype"] = "fp32"
-        if "bf16x3" in plan.describe:
-            # fp32 operands and accumulation; the GEMMs run on the bf16 matrix cores through an exact
-            # three-term split of each fp32 operand (DESIGN.md "bf16x3 split GEMMs")
-            out["roofline"]["gemm_form"] = "exact bf16x3 split of fp32 operands, fp32 accumulate"
+        if "bf16split" in plan.describe:
+            # fp32 operands and accumulation; the GEMMs run on the bf16 matrix cores through split
+            # operands (DESIGN.md "bf16 split GEMMs"): factors / dT in three round-to-nearest pieces
+            # (exact), the sample data in two (|x - x1 - x2| <= 2^-17 |x|) or three
+            xp = "three" if "xpieces=3" in plan.describe else "two"
+            out["roofline"]["gemm_form"] = (f"bf16 split GEMMs: factor-side operands in three RNE bf16 pieces, X in "
+                                            f"{xp}, fp32 accumulate")
     if rank_id == 0 and world == 1 and not args.no_cpu_baseline:
         log("cpu baseline ...")
         out["cpu_baseline"] = cpu_baseline(cfg, Xres, y, init, args.cpu_budget, args.cpu_threads)

@@ -250,12 +250,15 @@ int tr_adam_step_f64(tr_plan* plan, double* params, const double* grad, double* 
  *   slice-1pass-mfma   training at n_w = 256, 97 <= n_d <= 130 (n_d >= 128 or n_d % 4 == 0),
  *                      1 <= Rn <= 16, Rs * n_complex <= 16 with n_complex in {1, 2, 4},
  *                      n_out <= 64 (and its LDS fits): column-slice single pass (config 5);
- *                      described as slice-1pass-mfma-bf16x3 when its GEMMs run on the bf16 matrix
- *                      cores through an exact three-term split of the fp32 operands (the default;
- *                      fp32 accumulation; each product a.b is formed to < 2^-20 |ab| in the worst
- *                      case, typically 2^-25, against the f32 form's rounding of 2^-24, so results
- *                      are not bitwise those of the f32 MFMA form;
- *                      environment TR_SLICE_SPLIT=0 selects the f32 form)
+ *                      described as slice-1pass-mfma-bf16split when its GEMMs run on the bf16
+ *                      matrix cores through split operands (the default): factor-side operands in
+ *                      three round-to-nearest bf16 pieces (exact), the sample data in two
+ *                      (|x - x1 - x2| <= 2^-17 |x|, unbiased), fp32 accumulation.  At full config-5
+ *                      size its gradients lie within 3.5e-7 normwise of an fp64 closed form (the
+ *                      f32 MFMA form 1.1e-7, the reference's own fp32 op sequence 0.6-4.2e-6);
+ *                      results are not bitwise those of the f32 MFMA form.  Environment, read at
+ *                      plan creation: TR_SLICE_XPIECES=3 takes the sample data in three pieces too
+ *                      (exact; slower), TR_SLICE_SPLIT=0 the f32 MFMA form
  *   fused-1pass-mfma   K <= 32, n_w, n_d, n_out <= 256 and the whole sample + scratch in LDS:
  *                      single pass; also every tr_forward / tr_spectral_latents of such a plan
  *   generic-3kernel-mfma  any other shape in the envelope: T_n staged through HBM (three kernels)

@@ -42,7 +42,7 @@ struct SpecGeom {
   int gKP;  // K padded to 16 (row stride of the T / dT staging buffer)
   // column-slice training kernel (tr_spectral_slice.hip) for the shapes it covers (config 5)
   int sl;                       // 1: SPEC_TRAIN runs k_spec_slice
-  int slSp;                     // its GEMMs: 0 f32 MFMA, 1 exact bf16x3 split (lin packed), 2 split (lin unpacked)
+  int slSp;                     // its GEMMs: 0 f32 MFMA; bf16 split with X in two pieces: 1 lin packed, 2 not; X in three: 3, 4
   int slDt, sl_Dp;              // rows d >= 128 (<= 2), rows of the phi(A1) / phi(C1) tables
   int sl_oTail, sl_oEx, sl_oTP, sl_oPart, sl_oN1, sl_oLoss, sl_oPF, sl_lds_floats;  // LDS carve (floats)
 };

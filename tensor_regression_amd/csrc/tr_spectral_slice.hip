@@ -37,6 +37,7 @@
 
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 #include "tr_common.h"
 #include "tr_spectral.h"
@@ -72,6 +73,9 @@
 #ifndef TR_SLICE_BKW
 #define TR_SLICE_BKW 4  // wave that keeps the per-sample bookkeeping (dA2 / dC2 / bias / loss / y_hat,
                         // tail-row sums): a second-half wave, off the first half's critical path
+#endif
+#ifndef TR_SLICE_NOSEL
+#define TR_SLICE_NOSEL 1  // epilogue table reads without per-element lane masks (see tab8)
 #endif
 #ifndef TR_SLICE_PROFILE
 #define TR_SLICE_PROFILE 0  // profiling build: per-phase cycle counts of wave 0 of workgroups 0..255
@@ -111,47 +115,74 @@ constexpr int SL_SLICE = SL_ROWS * 32;  // floats of one wave's slice
 constexpr int SL_STEPS = SL_ROWS / 4;   // forward k steps per wave
 constexpr int SL_TILES = SL_ROWS / 16;  // gradient w tiles per wave
 constexpr int SL_TAIL = 64;             // tail floats per wave (Dt <= 2 rows x <= 32 w)
+// fixed part of the LDS carve (floats): slices, tails, exchange, tail partials, column partials;
+// compile-time in the kernel (held as run-time values they took scalar registers the sample loop
+// spilled); spec_slice_geom lays the same carve out
+constexpr int SL_O_TAIL = SL_NW * SL_SLICE;
+constexpr int SL_O_EX = SL_O_TAIL + SL_NW * SL_TAIL;
+constexpr int SL_O_TP = SL_O_EX + SL_NW * 64 * 8;
+constexpr int SL_O_PART = SL_O_TP + SL_NW * 64;
+constexpr int SL_O_N1 = SL_O_PART + SL_NW * 32;
 
 __device__ __forceinline__ sl_f4 sl_mfma(float a, float b, sl_f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
 // ---- exact three-term bf16 split (SP > 0) ---------------------------------------------------
-// x = x1 + x2 + x3 with x1 = x truncated to its top 8 significand bits, x2 = the top 8 bits of
-// the (exact) remainder, x3 = the rest (at most 8 significant bits: exactly a bf16).  A product
-// a.b is formed as the six cross terms of weight >= 2^-16 (a1b1, a1b2, a2b1, a1b3, a2b2, a3b1)
-// on v_mfma_f32_16x16x32_bf16 (16x the f32 MFMA rate); the dropped terms a2b3, a3b2, a3b3
-// weigh < 2^-20 |ab| in the worst case (truncation bounds |x2| < 2^-7 |x|, |x3| < 2^-14 |x|;
-// measured maximum 2^-21.3) and typically 2^-25, below the f32 rounding of the product (2^-24);
-// tests/test_split_numerics.py holds both bounds.
+// x = x1 + x2 + x3 by round-to-nearest-even bf16 conversions (v_cvt_pk_bf16_f32, two values per
+// instruction): x1 = bf16(x), r = x - x1 (exact: Sterbenz), x2 = bf16(r), x3 = r - x2 (exact, at
+// most 8 significant bits: exactly a bf16), for every finite |x| below the bf16 overflow
+// threshold (3.39e38) and above 2^-100.  |x2| <= 2^-8 |x|, |x3| <= 2^-17 |x|, and — unlike a
+// truncating split, whose pieces all carry the sign of x — the pieces' signs are independent of
+// x.  A product a.b is formed as the six cross terms of weight >= 2^-17 (a1b1, a1b2, a2b1, a1b3,
+// a2b2, a3b1) on v_mfma_f32_16x16x32_bf16 (16x the f32 MFMA rate), each exact in the fp32
+// accumulator; the dropped a2b3 + a3b2 + a3b3 weigh < 2^-24 |ab| (measured maximum 2^-24.3,
+// median 2^-29), below the fp32 rounding of the product itself, and have no bias toward the sign
+// of ab (a truncating split's dropped terms do: at config 5 that bias summed to 8-25x the f32
+// MFMA form's gradient error).  tests/test_split_numerics.py holds these bounds.
 typedef __bf16 sl_bf8 __attribute__((ext_vector_type(8)));
+typedef __bf16 sl_bf2 __attribute__((ext_vector_type(2)));
 typedef uint32_t sl_u4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ sl_f4 sl_mfma_bf(sl_u4 a, sl_u4 b, sl_f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(sl_bf8, a), __builtin_bit_cast(sl_bf8, b), c, 0,
                                                  0, 0);
 }
-#ifndef TR_SLICE_PK
-#define TR_SLICE_PK 0  // split remainders by packed-f32 subtractions (v_pk_add_f32)
-#endif
+// two values -> one VGPR of packed RNE bf16 (element 0 = a in the low half), v_cvt_pk_bf16_f32
+__device__ __forceinline__ uint32_t sl_pack_rne(float a, float b) {
+  return __builtin_bit_cast(uint32_t, sl_bf2{(__bf16)a, (__bf16)b});
+}
+// the two halves of a packed pair back as fp32 values (the low half by a byte permute: a shift of
+// the packed word lets the compiler re-convert that value alone, one more cvt per pair)
+__device__ __forceinline__ float sl_lo_f32(uint32_t h) { return __uint_as_float(__builtin_amdgcn_perm(h, h, 0x01000c0cu)); }
+__device__ __forceinline__ float sl_hi_f32(uint32_t h) { return __uint_as_float(h & 0xffff0000u); }
 // split a (element 2m) and b (element 2m+1) into the three packed bf16 pairs of VGPR m
-__device__ __forceinline__ void sl_split2(float a, float b, uint32_t& h1, uint32_t& h2, uint32_t& h3) {
-#if TR_SLICE_PK
-  const uint32_t ua = __float_as_uint(a), ub = __float_as_uint(b);
-  h1 = __builtin_amdgcn_perm(ub, ua, 0x07060302u);
-  const sl_f2 r = sl_f2{a, b} - sl_f2{__uint_as_float(ua & 0xffff0000u), __uint_as_float(ub & 0xffff0000u)};
-  const uint32_t ura = __float_as_uint(r.x), urb = __float_as_uint(r.y);
-  h2 = __builtin_amdgcn_perm(urb, ura, 0x07060302u);
-  const sl_f2 q = r - sl_f2{__uint_as_float(ura & 0xffff0000u), __uint_as_float(urb & 0xffff0000u)};
-  h3 = __builtin_amdgcn_perm(__float_as_uint(q.y), __float_as_uint(q.x), 0x07060302u);
-#else
-  const uint32_t ua = __float_as_uint(a), ub = __float_as_uint(b);
-  h1 = __builtin_amdgcn_perm(ub, ua, 0x07060302u);
-  const float ra = a - __uint_as_float(ua & 0xffff0000u), rb = b - __uint_as_float(ub & 0xffff0000u);
-  const uint32_t ura = __float_as_uint(ra), urb = __float_as_uint(rb);
-  h2 = __builtin_amdgcn_perm(urb, ura, 0x07060302u);
-  const float sa = ra - __uint_as_float(ura & 0xffff0000u), sb = rb - __uint_as_float(urb & 0xffff0000u);
-  h3 = __builtin_amdgcn_perm(__float_as_uint(sb), __float_as_uint(sa), 0x07060302u);
+#ifndef TR_SLICE_SPLITMODE
+#define TR_SLICE_SPLITMODE 2  // 2: x1, x2, x3 all by round-to-nearest (above); 1: x1 truncated, x2 / x3 by
+                              // round-to-nearest (unbiased too, dropped terms < 2^-22 |ab|); 0: all
+                              // truncated (round 3: dropped terms biased toward the sign of ab)
 #endif
+__device__ __forceinline__ void sl_split2(float a, float b, uint32_t& h1, uint32_t& h2, uint32_t& h3) {
+  float ra, rb;
+  if (TR_SLICE_SPLITMODE == 2) {
+    h1 = sl_pack_rne(a, b);
+    ra = a - sl_lo_f32(h1);
+    rb = b - sl_hi_f32(h1);
+  } else {
+    const uint32_t ua = __float_as_uint(a), ub = __float_as_uint(b);
+    h1 = __builtin_amdgcn_perm(ub, ua, 0x07060302u);
+    ra = a - __uint_as_float(ua & 0xffff0000u);
+    rb = b - __uint_as_float(ub & 0xffff0000u);
+  }
+  if (TR_SLICE_SPLITMODE == 0) {
+    const uint32_t ura = __float_as_uint(ra), urb = __float_as_uint(rb);
+    h2 = __builtin_amdgcn_perm(urb, ura, 0x07060302u);
+    const float sa = ra - __uint_as_float(ura & 0xffff0000u), sb = rb - __uint_as_float(urb & 0xffff0000u);
+    h3 = __builtin_amdgcn_perm(__float_as_uint(sb), __float_as_uint(sa), 0x07060302u);
+    return;
+  }
+  h2 = sl_pack_rne(ra, rb);
+  const float sa = ra - sl_lo_f32(h2), sb = rb - sl_hi_f32(h2);
+  h3 = sl_pack_rne(sa, sb);
 }
 __device__ __forceinline__ void sl_split_m(float a, float b, sl_u4 (&f)[3], int m) {
   uint32_t h1, h2, h3;
@@ -160,26 +191,27 @@ __device__ __forceinline__ void sl_split_m(float a, float b, sl_u4 (&f)[3], int 
   f[1][m] = h2;
   f[2][m] = h3;
 }
-#ifndef TR_SLICE_X2
-#define TR_SLICE_X2 0  // experiment build only: the X side (first operand at every call site) as
-                       // two round-to-nearest bf16 pieces (NOT exact: representation error up to
-                       // 2^-16 |x|, median 2^-19.4): five / three MFMAs per product
-#endif
-// X-side split: three exact pieces, or with TR_SLICE_X2 two round-to-nearest ones (x3 unused)
+// X side (the first operand at every call site: the sample data) in XP pieces.  XP = 2 (the
+// default): x = x1 + x2 + e by two round-to-nearest bf16 conversions, |e| <= 2^-17 |x| with no
+// bias (e's sign is independent of x's); five MFMAs per product of the six-term form and three
+// of the packed-lin form, 6 VALU per pair of values instead of 11.  XP = 3: the three-piece split
+// above, x represented exactly.  Measured at full config-5 size against an fp64 closed form
+// (tests/test_gpu_fullsize.py), both forms' gradients sit within 1.7-3.5e-7 normwise, the f32
+// MFMA form's within 1.1e-7 and the reference's own fp32 op sequence on the CPU within 0.6-4.2e-6.
+template <int XP>
 __device__ __forceinline__ void sl_splitx_m(float a, float b, sl_u4 (&f)[3], int m) {
-#if TR_SLICE_X2
-  typedef __bf16 sl_bf2 __attribute__((ext_vector_type(2)));
-  const uint32_t h1 = __builtin_bit_cast(uint32_t, sl_bf2{(__bf16)a, (__bf16)b});
-  const float ra = a - __uint_as_float(h1 << 16), rb = b - __uint_as_float(h1 & 0xffff0000u);
-  f[0][m] = h1;
-  f[1][m] = __builtin_bit_cast(uint32_t, sl_bf2{(__bf16)ra, (__bf16)rb});
-#else
-  sl_split_m(a, b, f, m);
-#endif
+  if constexpr (XP == 2) {
+    const uint32_t h1 = sl_pack_rne(a, b);
+    f[0][m] = h1;
+    f[1][m] = sl_pack_rne(a - sl_lo_f32(h1), b - sl_hi_f32(h1));
+  } else {
+    sl_split_m(a, b, f, m);
+  }
 }
-// c += A.B over the six cross terms (A, B each as three split fragments)
+// c += A.B over the six cross terms of weight >= 2^-17 (A in XP pieces, B in three)
+template <int XP>
 __device__ __forceinline__ sl_f4 sl_mfma6(const sl_u4 (&a)[3], const sl_u4 (&b)[3], sl_f4 c) {
-  if (!TR_SLICE_X2) c = sl_mfma_bf(a[2], b[0], c);
+  if constexpr (XP == 3) c = sl_mfma_bf(a[2], b[0], c);
   c = sl_mfma_bf(a[1], b[1], c);
   c = sl_mfma_bf(a[0], b[2], c);
   c = sl_mfma_bf(a[1], b[0], c);
@@ -189,14 +221,19 @@ __device__ __forceinline__ sl_f4 sl_mfma6(const sl_u4 (&a)[3], const sl_u4 (&b)[
 }
 // packed lin columns (Rn <= 8): B = [b1 | b2] (lanes 0-7 | 8-15) and [b3 | 0]; column c of the
 // product is the sum of accumulator columns c and c + 8 (folded by sl_fold8): four MFMAs for
-// the six cross terms (a3b2 comes along)
+// the six cross terms (a3b2 comes along), three with a two-piece A
+template <int XP>
 __device__ __forceinline__ sl_f4 sl_mfma_lp(const sl_u4 (&a)[3], const sl_u4 (&b)[2], sl_f4 c) {
-  if (!TR_SLICE_X2) c = sl_mfma_bf(a[2], b[0], c);
+  if constexpr (XP == 3) c = sl_mfma_bf(a[2], b[0], c);
   c = sl_mfma_bf(a[0], b[1], c);
   c = sl_mfma_bf(a[1], b[0], c);
   c = sl_mfma_bf(a[0], b[0], c);
   return c;
 }
+// SP (the kernel's GEMM form): 0 f32 MFMA; 1 / 2 bf16 split with a two-piece X, lin columns
+// packed (Rn <= 8) / not; 3 / 4 the same with the three-piece X
+#define SL_LP(SP) ((SP) == 1 || (SP) == 3)
+#define SL_XP(SP) ((SP) >= 3 ? 3 : 2)
 template <int CTRL>
 __device__ __forceinline__ float sl_dpp(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
@@ -271,6 +308,14 @@ __device__ __forceinline__ void sl_wait_vm(int n) {
 #undef SL_VM8
 #undef SL_VM
 }
+// this lane's index recomputed where it is used (v_mbcnt, not a register held across the sample
+// loop: at 256 VGPRs the compiler spilled the held lane index, and each reload's vmcnt(0) wait
+// drained the in-flight LDS-DMA of the next sample); volatile, so it is neither hoisted nor shared
+__device__ __forceinline__ int sl_lane_now() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
 // slot xor of chunk r (x = r & 7: bit 0 -> bit 0, bit 1 -> bit 2)
 __device__ __forceinline__ int sl_swz(int x) { return (x & 1) | ((x & 2) << 1); }
 }  // namespace
@@ -304,12 +349,12 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
   const bool vlane = rs_ok && (i % CC) == 0;  // lane that carries V / dPhi(C1) of rank rs
 
   float* slice = lds + wv * SL_SLICE;
-  float* sTail = lds + g.sl_oTail + wv * SL_TAIL;  // [Dt][TR]
-  float* sEx = lds + g.sl_oEx;                      // [8 waves][64 lanes][8]
-  float* sTP = lds + g.sl_oTP;                      // [8 waves][2 rows][32 columns]
-  float* sPart = lds + g.sl_oPart;                  // [8 waves][Z 16 | V 16]
+  float* sTail = lds + SL_O_TAIL + wv * SL_TAIL;  // [Dt][TR]
+  float* sEx = lds + SL_O_EX;                      // [8 waves][64 lanes][8]
+  float* sTP = lds + SL_O_TP;                      // [8 waves][2 rows][32 columns]
+  float* sPart = lds + SL_O_PART;                  // [8 waves][Z 16 | V 16]
   const int Dp = g.sl_Dp;                           // table row length (>= max(D, 128), % 4 == 0)
-  float* sN1 = lds + g.sl_oN1;                      // [Rn][Dp] phi(A1)^T (d contiguous: b128 reads)
+  float* sN1 = lds + SL_O_N1;                       // [Rn][Dp] phi(A1)^T (d contiguous: b128 reads)
   float* sC1 = sN1 + Dp * Rn;                       // [Rs][Dp] phi(C1)^T
   float* sCA = sC1 + g.sl_Dp * Rs;                  // [NO][16] w_r phi(A2)
   float* sCC = sCA + NO * 16;                       // [NO][16] phi(C2)
@@ -319,7 +364,7 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
   float* sTacc = sAcc + NO * (Rn + Rs + 1);         // bookkeeping wave: [Dt][dPhi(A1) 16 | dPhi(C1) 16] of rows 128+
   double* sLoss = reinterpret_cast<double*>(lds + g.sl_oLoss);  // bookkeeping wave lane 0: sum of squared errors
 
-  for (int e = g.sl_oTail + t; e < g.sl_lds_floats; e += SL_T) lds[e] = 0.f;
+  for (int e = SL_O_TAIL + t; e < g.sl_lds_floats; e += SL_T) lds[e] = 0.f;
   __syncthreads();
   for (int e = t; e < D * Rn; e += SL_T) sN1[(e % Rn) * Dp + e / Rn] = phi[g.offA1 + e];
   for (int e = t; e < D * Rs; e += SL_T) sC1[(e % Rs) * Dp + e / Rs] = phi[g.offC1 + e];
@@ -338,7 +383,7 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
   // split mode: k step S covers steps 8S .. 8S+7 (element j of lane group gq <-> w = 32 S + 4 j
   // + gq of the half, the same w for A and B); bs = spectral columns, bl = lin columns
   constexpr int NSP = SP ? SL_STEPS / 8 : 1;
-  constexpr int NL = SP == 2 ? 3 : 2;
+  constexpr int NL = SL_LP(SP) ? 2 : 3;
   sl_u4 bs[NSP][3], bl[NSP][NL];
   if constexpr (!SP) {
 #pragma unroll
@@ -348,7 +393,7 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
       bf1[s] = i < Rn ? Phi0[w * K + i] : 0.f;
     }
   } else {
-    const int cl = SP == 1 ? (i & 7) : i;  // lin column this lane splits
+    const int cl = SL_LP(SP) ? (i & 7) : i;  // lin column this lane splits
 #pragma unroll
     for (int S = 0; S < NSP; ++S)
 #pragma unroll
@@ -357,7 +402,7 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
         sl_split_m(i < RC ? Phi0[w0 * K + Rn + i] : 0.f, i < RC ? Phi0[w1 * K + Rn + i] : 0.f, bs[S], m);
         uint32_t h1, h2, h3;
         sl_split2(cl < Rn ? Phi0[w0 * K + cl] : 0.f, cl < Rn ? Phi0[w1 * K + cl] : 0.f, h1, h2, h3);
-        if constexpr (SP == 1) {
+        if constexpr (SL_LP(SP)) {
           bl[S][0][m] = i < 8 ? h1 : h2;
           bl[S][1][m] = i < 8 ? h3 : 0u;
         } else {
@@ -382,15 +427,17 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
   const float bm = (float)((Rn > 0) + (Rs > 0));  // the bias is added by both terms (Q10)
 
   // per-lane LDS offsets (floats) of the forward operand (step s: + 128 s, period 4 in the
-  // swizzle) and of the two gradient operand reads (tile q: + 512 q)
-  int fo[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const int r = 2 * s + (gq >> 1);
-    fo[s] = 64 * (gq >> 1) + 4 * (((i >> 1) + 8 * (gq & 1)) ^ sl_swz(r)) + 2 * (i & 1);
-  }
-  const int bo0 = 64 * (i >> 1) + 4 * ((2 * gq + 0 + 8 * (i & 1)) ^ sl_swz(i >> 1));
-  const int bo1 = 64 * (i >> 1) + 4 * ((2 * gq + 1 + 8 * (i & 1)) ^ sl_swz(i >> 1));
+  // swizzle) and of the two gradient operand reads (tile q: + 512 q); formed from a fresh lane
+  // index at the phase that uses them (held across the sample loop they took registers the
+  // split GEMMs need)
+  auto fo_of = [](int L, int s) {
+    const int i = L & 15, gq = L >> 4, r = 2 * s + (gq >> 1);
+    return 64 * (gq >> 1) + 4 * (((i >> 1) + 8 * (gq & 1)) ^ sl_swz(r)) + 2 * (i & 1);
+  };
+  auto bo_of = [](int L, int c) {
+    const int i = L & 15, gq = L >> 4;
+    return 64 * (i >> 1) + 4 * ((2 * gq + c + 8 * (i & 1)) ^ sl_swz(i >> 1));
+  };
 
   const int64_t n0 = (int64_t)blockIdx.x * rows_per_wg;
   const int64_t n1 = n0 + rows_per_wg < N ? n0 + rows_per_wg : N;
@@ -407,16 +454,20 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
   // The lane part of a piece's source is the same for every tile and sample: two byte offsets
   // (c4 = 0, 1) held for the launch; the sample base goes into a buffer descriptor (SGPRs) and
   // the tile's row offset into soffset, so a piece costs no per-lane address arithmetic.
-  uint32_t dvo[2];
-#pragma unroll
-  for (int c4 = 0; c4 < 2; ++c4) {
-    const int lsl = lane & 15, lc = lane >> 4;
+  auto dvo_of = [&](int L, int c4) {
+    const int lsl = L & 15, lc = L >> 4;
     const int x = 4 * c4 + lc;  // chunk within the tile (= r & 7)
     const int sp = lsl ^ sl_swz(x);
     int d = dbase + 4 * (sp & 7);
     d = d < D ? d : 0;  // a column quad past D (D < 128, D % 4 == 0): any valid quad, times zero
-    dvo[c4] = (uint32_t)(((2 * x + (sp >> 3)) * D + d) * 4);
-  }
+    return (uint32_t)(((2 * x + (sp >> 3)) * D + d) * 4);
+  };
+  uint32_t dvo[2];  // (set by the phase that issues pieces)
+  auto set_dvo = [&]() {
+    const int L = sl_lane_now();
+    dvo[0] = dvo_of(L, 0);
+    dvo[1] = dvo_of(L, 1);
+  };
   const uint32_t sbytes = (uint32_t)(g.W * D * 4);
   auto rsrc_of = [&](int64_t n) {
     const uint64_t a = (uint64_t)(uintptr_t)(X + n * xld);
@@ -433,8 +484,7 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
     dma_piece(n, q, 1);
   };
   auto dma_tail = [&](int64_t n) {
-    int ln = lane;  // opaque copy: the per-lane source is formed at the call (no live address pair)
-    asm volatile("" : "+v"(ln));
+    const int ln = sl_lane_now();  // the per-lane source is formed at the call (no live address pair)
     if (ln < Dt * TR) {  // lane -> (row 128 + lane / TR, w offset lane % TR)
       const int tr = ln / TR, wo = ln - tr * TR;
       const int64_t w = wbase + TR * p + wo;
@@ -456,8 +506,7 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
   // sample's transfer could only overlap the gradient GEMM.)
   constexpr int NPF = SP ? TR_SLICE_PF : 0;
   auto prefetch = [&](int64_t n) {
-    int ln = lane;
-    asm volatile("" : "+v"(ln));
+    const int ln = sl_lane_now();
     const int64_t sbytes = (int64_t)g.W * D * 4;
     const char* base = reinterpret_cast<const char*>(X + n * xld);
 #pragma unroll
@@ -467,6 +516,7 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
       sl_dma4(reinterpret_cast<const float*>(base + off), lds + g.sl_oPF);
     }
   };
+  set_dvo();
   if (nr > 0) dma_sample(sample_of(0));
   if (TR_SLICE_PRIO == 1 && hw == 1) __builtin_amdgcn_s_setprio(1);
   if (TR_SLICE_PRIO == 2 && hw == 0) __builtin_amdgcn_s_setprio(1);
@@ -493,6 +543,12 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
     {
       sl_f2 xa[4], xb[4];
       sl_u4 xf[2][3];  // split mode: the k step's A fragments of d tiles 0 / 1
+      int fo[4];
+      {
+        const int L = sl_lane_now();
+#pragma unroll
+        for (int s = 0; s < 4; ++s) fo[s] = fo_of(L, s);
+      }
       {
         SL_SUB_BEGIN();
         sl_wait_vm((ntl - 1) * 2 + npf);
@@ -524,19 +580,19 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
           // tile q holds elements 4 (q & 1) .. +3 of k step q / 2: VGPRs 2 (q & 1), 2 (q & 1) + 1
 #pragma unroll
           for (int mm = 0; mm < 2; ++mm) {
-            sl_splitx_m(xa[2 * mm].x, xa[2 * mm + 1].x, xf[0], 2 * (q & 1) + mm);
-            sl_splitx_m(xa[2 * mm].y, xa[2 * mm + 1].y, xf[1], 2 * (q & 1) + mm);
+            sl_splitx_m<SL_XP(SP)>(xa[2 * mm].x, xa[2 * mm + 1].x, xf[0], 2 * (q & 1) + mm);
+            sl_splitx_m<SL_XP(SP)>(xa[2 * mm].y, xa[2 * mm + 1].y, xf[1], 2 * (q & 1) + mm);
           }
           if ((q & 1) && !(TR_SLICE_SKIP & 2)) {
             const int S = q >> 1;
-            T00 = sl_mfma6(xf[0], bs[S], T00);
-            T01 = sl_mfma6(xf[1], bs[S], T01);
-            if constexpr (SP == 1) {
-              T10 = sl_mfma_lp(xf[0], bl[S], T10);
-              T11 = sl_mfma_lp(xf[1], bl[S], T11);
+            T00 = sl_mfma6<SL_XP(SP)>(xf[0], bs[S], T00);
+            T01 = sl_mfma6<SL_XP(SP)>(xf[1], bs[S], T01);
+            if constexpr (SL_LP(SP)) {
+              T10 = sl_mfma_lp<SL_XP(SP)>(xf[0], bl[S], T10);
+              T11 = sl_mfma_lp<SL_XP(SP)>(xf[1], bl[S], T11);
             } else {
-              T10 = sl_mfma6(xf[0], bl[S], T10);
-              T11 = sl_mfma6(xf[1], bl[S], T11);
+              T10 = sl_mfma6<SL_XP(SP)>(xf[0], bl[S], T10);
+              T11 = sl_mfma6<SL_XP(SP)>(xf[1], bl[S], T11);
             }
           }
         }
@@ -566,13 +622,12 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
     // lane-dependent indices of the epilogue from an opaque copy of the lane index: every LDS
     // address below is then formed here (a few VALU ops) instead of living across the loop
     // (held through the GEMMs, the split kernels spilled them to scratch: a vmcnt(0) reload each)
-    int lk = lane;
-    asm volatile("" : "+v"(lk));
+    const int lk = sl_lane_now();
     const int i = lk & 15, gq = lk >> 4;
     const int rs = i / CC;
     const bool rs_ok = rs < Rs;
     const bool vlane = rs_ok && (i % CC) == 0;
-    if constexpr (SP == 1) {  // packed lin columns: column c = accumulator columns c + (c ^ 8)
+    if constexpr (SL_LP(SP)) {  // packed lin columns: column c = accumulator columns c + (c ^ 8)
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
         T10[v] = sl_fold8(T10[v]);
@@ -589,14 +644,14 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
         for (int m = 0; m < 4; ++m) {
           const float x0 = i < Dt ? sTail[i * TR + 8 * m + gq] : 0.f;
           const float x1 = i < Dt ? sTail[i * TR + 8 * m + 4 + gq] : 0.f;
-          sl_splitx_m(x0, x1, tf, m);
+          sl_splitx_m<SL_XP(SP)>(x0, x1, tf, m);
         }
         auto tail_step = [&](const sl_u4(&b_s)[3], const sl_u4(&b_l)[NL]) {
-          Tts = sl_mfma6(tf, b_s, Tts);
-          if constexpr (SP == 1)
-            Ttl = sl_mfma_lp(tf, b_l, Ttl);
+          Tts = sl_mfma6<SL_XP(SP)>(tf, b_s, Tts);
+          if constexpr (SL_LP(SP))
+            Ttl = sl_mfma_lp<SL_XP(SP)>(tf, b_l, Ttl);
           else
-            Ttl = sl_mfma6(tf, b_l, Ttl);
+            Ttl = sl_mfma6<SL_XP(SP)>(tf, b_l, Ttl);
         };
         switch (p) {
           case 0: tail_step(bs[0], bl[0]); break;
@@ -611,7 +666,7 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
       for (int tr = 0; tr < Dt; ++tr) {
         if constexpr (SP) {
           ta[tr][0] = Tts[tr];
-          ta[tr][1] = SP == 1 ? sl_fold8(Ttl[tr]) : Ttl[tr];
+          ta[tr][1] = SL_LP(SP) ? sl_fold8(Ttl[tr]) : Ttl[tr];
         } else {
           ta[tr][0] = sl_groups_sum(ta[tr][0]);
           ta[tr][1] = sl_groups_sum(ta[tr][1]);
@@ -656,18 +711,23 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
     };
     // table offsets from an opaque copy of the lane index: recomputed here (a few VALU ops)
     // instead of living across the sample loop as spilled registers
-    int lo = lk;
-    asm volatile("" : "+v"(lo));
+    const int lo = sl_lane_now();
     const int ie = lo & 15, ge = lo >> 4, rse = ie / CC;
     // phi(A1)[d, ie] / phi(C1)[d, ie / CC] of this lane's 8 rows d = dbase + 8 ge + 2v + h: two
     // ds_read_b128 each, element 2v + h
     const int n1o = (ie < Rn ? ie : 0) * Dp + dbase + 8 * ge, c1o = (rse < Rs ? rse : 0) * Dp + dbase + 8 * ge;
+    // (TR_SLICE_NOSEL: no per-element lane masks; a lane past Rn / Rs reads table row 0, finite,
+    // and meets zero factors: T columns past Rn are zero, and dz / dv are zeroed there, so only
+    // the lin column partial needs one mask — the packed form's lanes 8-15 hold folded columns)
     auto tab8 = [&](const float* tb, int off, bool ok, float (&o)[2][4]) {
       const sl_f4 lo = *reinterpret_cast<const sl_f4*>(tb + off), hi = *reinterpret_cast<const sl_f4*>(tb + off + 4);
 #pragma unroll
       for (int v = 0; v < 4; ++v)
 #pragma unroll
-        for (int h = 0; h < 2; ++h) o[h][v] = ok ? (v < 2 ? lo[2 * v + h] : hi[2 * (v - 2) + h]) : 0.f;
+        for (int h = 0; h < 2; ++h) {
+          const float x = v < 2 ? lo[2 * v + h] : hi[2 * (v - 2) + h];
+          o[h][v] = (TR_SLICE_NOSEL || ok) ? x : 0.f;
+        }
     };
     float zp = 0.f, vp = 0.f;
     {
@@ -683,6 +743,7 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
         vp = fmaf(hw == 0 ? c1[0][v] : c1[1][v], norm_of(hw == 0 ? T00[v] : T01[v]), vp);
     }
     vp = vlane ? vp : 0.f;
+    if (TR_SLICE_NOSEL) zp = i < Rn ? zp : 0.f;
     const float Mt = norm_of(tt0);
     const int dtl = 128 + gq;  // tail row of this lk group (valid when gq < Dt)
     const float n1t = (Dt > 0 && gq < Dt && i < Rn) ? sN1[i * Dp + dtl] : 0.f;
@@ -771,6 +832,13 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
       float at[TQ];
 #pragma unroll
       for (int u = 0; u < TQ; ++u) at[u] = (Dt > 0 && gq < Dt) ? sTail[gq * TR + 16 * u + i] : 0.f;
+      set_dvo();
+      int bo0, bo1;
+      {
+        const int L = sl_lane_now();
+        bo0 = bo_of(L, 0);
+        bo1 = bo_of(L, 1);
+      }
       if (has_next && Dt > 0) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         dma_tail(nn);
@@ -784,7 +852,7 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
           sl_split_m(T00[v], T01[v], ds, v);
           uint32_t h1, h2, h3;
           sl_split2(T10[v], T11[v], h1, h2, h3);
-          if constexpr (SP == 1) {  // lanes 8-15 take the second part of column i - 8
+          if constexpr (SL_LP(SP)) {  // lanes 8-15 take the second part of column i - 8
             const uint32_t h2r = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)h2, 0x128, 0xF, 0xF, false);
             dl[0][v] = i < 8 ? h1 : h2r;
             dl[1][v] = i < 8 ? h3 : 0u;
@@ -840,19 +908,19 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
 #pragma unroll
             for (int v = 0; v < 4; ++v) {
               const sl_f4& src = v < 2 ? va : vb;
-              sl_splitx_m(src[2 * (v & 1) + 0], src[2 * (v & 1) + 1], af, v);
+              sl_splitx_m<SL_XP(SP)>(src[2 * (v & 1) + 0], src[2 * (v & 1) + 1], af, v);
             }
             if (has_next) {
               asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // tile q's reads landed
               dma_piece(nn, q, 0);
             }
-            if (!(TR_SLICE_SKIP & 4)) gacc[q][0] = sl_mfma6(af, ds, gacc[q][0]);
+            if (!(TR_SLICE_SKIP & 4)) gacc[q][0] = sl_mfma6<SL_XP(SP)>(af, ds, gacc[q][0]);
             if (has_next) dma_piece(nn, q, 1);
             if (!(TR_SLICE_SKIP & 4)) {
-              if constexpr (SP == 1)
-                gacc[q][1] = sl_mfma_lp(af, dl, gacc[q][1]);
+              if constexpr (SL_LP(SP))
+                gacc[q][1] = sl_mfma_lp<SL_XP(SP)>(af, dl, gacc[q][1]);
               else
-                gacc[q][1] = sl_mfma6(af, dl, gacc[q][1]);
+                gacc[q][1] = sl_mfma6<SL_XP(SP)>(af, dl, gacc[q][1]);
             }
           }
           if (Dt > 0 && q / TQ == p) {
@@ -871,7 +939,7 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
 #endif
   // ---- per-workgroup slab (arena layout, phi space) -------------------------------------------
   __syncthreads();  // (no LDS-DMA in flight: the last sample issued none)
-  if constexpr (SP == 1) {  // packed lin columns
+  if constexpr (SL_LP(SP)) {  // packed lin columns
 #pragma unroll
     for (int q = 0; q < SL_TILES; ++q)
 #pragma unroll
@@ -944,15 +1012,18 @@ void spec_slice_geom(SpecGeom* g) {
   const int Dt = g->D > 128 ? g->D - 128 : 0;
   if (g->NO > 64) return;
   g->slDt = Dt;
-  // GEMMs on the bf16 matrix cores through the exact three-term split unless TR_SLICE_SPLIT=0
+  // GEMMs on the bf16 matrix cores through split operands: X in two pieces (default) or three
+  // (TR_SLICE_XPIECES=3); TR_SLICE_SPLIT=0 keeps the f32 MFMA form
   const char* spl = std::getenv("TR_SLICE_SPLIT");
-  g->slSp = (spl != nullptr && spl[0] == '0') ? 0 : (g->Rn <= 8 ? 1 : 2);
+  const char* xpc = std::getenv("TR_SLICE_XPIECES");
+  const int x3 = (xpc != nullptr && xpc[0] == '3') ? 2 : 0;
+  g->slSp = (spl != nullptr && spl[0] == '0') ? 0 : (g->Rn <= 8 ? 1 : 2) + x3;
   g->sl_Dp = ((g->D > 128 ? g->D : 128) + 3) & ~3;
-  g->sl_oTail = SL_NW * SL_SLICE;
-  g->sl_oEx = g->sl_oTail + SL_NW * SL_TAIL;
-  g->sl_oTP = g->sl_oEx + SL_NW * TR_WAVE * 8;
-  g->sl_oPart = g->sl_oTP + SL_NW * 64;
-  g->sl_oN1 = g->sl_oPart + SL_NW * 32;
+  g->sl_oTail = SL_O_TAIL;
+  g->sl_oEx = SL_O_EX;
+  g->sl_oTP = SL_O_TP;
+  g->sl_oPart = SL_O_PART;
+  g->sl_oN1 = SL_O_N1;
   const int64_t small = (int64_t)g->sl_Dp * (g->Rn + g->Rs) + (int64_t)g->NO * 33 + 16 +
                         (int64_t)g->NO * (g->Rn + g->Rs + 1) + 2 * 32;
   g->sl_oLoss = (int)(g->sl_oN1 + ((small + 3) & ~(int64_t)3));  // 16-B aligned double
@@ -964,7 +1035,7 @@ void spec_slice_geom(SpecGeom* g) {
 }
 
 template <int DT, int SP>
-static const void* slice_kernel_dt(int cc) {
+static const void* slice_kernel_dt(int cc) {  // (cc: 1, 2 or 4)
   if (cc == 1) return reinterpret_cast<const void*>(&k_spec_slice<1, DT, SP>);
   if (cc == 2) return reinterpret_cast<const void*>(&k_spec_slice<2, DT, SP>);
   return reinterpret_cast<const void*>(&k_spec_slice<4, DT, SP>);
@@ -974,7 +1045,13 @@ static const void* slice_kernel_sp(int cc, int dt) {
   return dt == 0 ? slice_kernel_dt<0, SP>(cc) : (dt == 1 ? slice_kernel_dt<1, SP>(cc) : slice_kernel_dt<2, SP>(cc));
 }
 static const void* slice_kernel(int cc, int dt, int sp) {
-  return sp == 0 ? slice_kernel_sp<0>(cc, dt) : (sp == 1 ? slice_kernel_sp<1>(cc, dt) : slice_kernel_sp<2>(cc, dt));
+  switch (sp) {
+    case 0: return slice_kernel_sp<0>(cc, dt);
+    case 1: return slice_kernel_sp<1>(cc, dt);
+    case 2: return slice_kernel_sp<2>(cc, dt);
+    case 3: return slice_kernel_sp<3>(cc, dt);
+    default: return slice_kernel_sp<4>(cc, dt);
+  }
 }
 
 hipError_t spec_slice_prepare(SpecGeom* g) {

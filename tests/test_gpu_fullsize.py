@@ -8,7 +8,9 @@ properties that hold at any size:
     LOSS_TOL and every factor gradient to GRAD_TOL normwise — tolerances set from the measured
     error with a margin (the fp32 reference itself sits ~1e-6..1e-5 from fp64 at these sizes,
     SURVEY.md §8(c));
-  * config 5 (spectral): the full-size gradient equals the sum of the two half-shard gradients
+  * config 5 (spectral): the same fp64 comparison on the product kernel (k_spec_slice's bf16
+    split GEMMs) and on its f32-MFMA form, both held to twice the error of the reference's own
+    op sequence run in fp32 on the host CPU; and properties: the full-size gradient equals the sum of the two half-shard gradients
     (linearity over samples), calls of equal traversal parity are bitwise identical, and the
     first loss fit_Adam logs is the loss of one loss_grad + finalize_grad at the same factors.
 Inputs are generated on the device from fixed seeds (same recipe as bench.py).
@@ -262,35 +264,93 @@ def _spectral_fp64(X, y, Bn, Bc, bias, lam):
     return data, data + lam * pen, grads, gb
 
 
+
+
+def _spectral_errs(X, y, split):
+    """Full-size loss + gradient of one slice-kernel form against the fp64 closed form."""
+    import os
+    from tensor_regression_amd import spectral_tensor_regression as SP
+    N, W, D = X.shape
+    O = y.shape[1]
+    old = os.environ.pop("TR_SLICE_SPLIT", None)
+    if not split:
+        os.environ["TR_SLICE_SPLIT"] = "0"
+    SP._plan_cache.clear()
+    try:
+        torch.manual_seed(1)
+        model = SP.CP_linear_regression(X.shape, y.shape, rank_normal=8, rank_spectral=8, n_complex_dim=1,
+                                        device=DEV)
+        plan = model._get_plan(X, N)
+        arena = plan.pack(model.Bcp_n, model.Bcp_c, model.bias)
+        w = torch.ones(16, device=DEV)
+        lam = 0.01
+        grad = torch.zeros(plan.num_grads, device=DEV)
+        gtot = torch.zeros(plan.num_params, device=DEV)
+        loss = torch.zeros(1, device=DEV)
+        plan.loss_grad(X, y, None, float(N * O), arena, w, grad)
+        plan.finalize_grad(arena, grad, lam, gtot, loss)
+        data, total, grads, gb = _spectral_fp64(X, y, model.Bcp_n, model.Bcp_c, model.bias, lam)
+        errs = {"data_loss": abs(grad[plan.num_params].item() - data) / abs(data),
+                "loss": abs(loss.item() - total) / abs(total),
+                "bias": normwise_rel(gtot[plan.offsets[6]:].cpu().numpy(), gb.cpu().numpy())}
+        for f, (v, ref) in enumerate(zip(plan.factor_views(gtot), grads)):
+            errs[f"grad{f}"] = normwise_rel(v.cpu().numpy(), ref.cpu().numpy())
+        return plan.describe, errs
+    finally:
+        os.environ.pop("TR_SLICE_SPLIT", None)
+        if old is not None:
+            os.environ["TR_SLICE_SPLIT"] = old
+        SP._plan_cache.clear()
+
+
+def _spectral_ref32_errs(X, y, lam=0.01):
+    """The reference's own op sequence (oracle.cp_oracle.spectral_loss_grad: lin_model through
+    cp_to_tensor + inner, stepwise_spectral_model through torch.einsum + norm, MSELoss, autograd;
+    spectral_tensor_regression.py:118-165, 339-390, 714-720) in fp32 on the host CPU, at the same
+    factors, against the same fp64 closed form: the error an fp32 implementation of the
+    reference makes at this size."""
+    import os
+    from oracle import cp_oracle
+    from tensor_regression_amd import spectral_tensor_regression as SP
+    N, W, D = X.shape
+    torch.manual_seed(1)
+    model = SP.CP_linear_regression(X.shape, y.shape, rank_normal=8, rank_spectral=8, n_complex_dim=1, device=DEV)
+    Bn = [a.detach().cpu() for a in model.Bcp_n]
+    Bc = [a.detach().cpu() for a in model.Bcp_c]
+    b = model.bias.detach().cpu()
+    quota = os.environ.get("OMP_NUM_THREADS")
+    torch.set_num_threads(int(quota) if quota and quota.isdigit() else min(16, os.cpu_count() or 1))
+    r = cp_oracle.spectral_loss_grad(X.cpu(), y.cpu(), Bn, Bc, b, torch.ones(16), 8, [False] * 3, lam)
+    data, total, grads, gb = _spectral_fp64(X, y, model.Bcp_n, model.Bcp_c, model.bias, lam)
+    errs = {"data_loss": abs(r["data_loss"] - data) / abs(data), "loss": abs(r["loss"] - total) / abs(total),
+            "bias": normwise_rel(r["bias_grad"], gb.cpu().numpy())}
+    for f, (v, ref) in enumerate(zip(r["grads_n"] + r["grads_c"], grads)):
+        errs[f"grad{f}"] = normwise_rel(v, ref.cpu().numpy())
+    return errs
+
+
 def test_spectral_full_size_vs_fp64():
     """Config 5 at full size (X (32768, 256, 129), rank_normal = rank_spectral = 8, n_complex_dim 1,
-    y (N, 2)) on the product kernel (k_spec_slice, exact bf16x3 split GEMMs) against the fp64
-    closed form: the same bar as configs 2-4."""
-    from tensor_regression_amd.spectral_tensor_regression import CP_linear_regression
+    y (N, 2)) against the fp64 closed form, on the product kernel (k_spec_slice, bf16 split
+    GEMMs), on its f32-MFMA form (TR_SLICE_SPLIT=0) and on the reference's own op sequence in fp32
+    on the host CPU (the oracle).  Bar, as for every long-horizon check in this suite: no further
+    from fp64 than the reference's own fp32 computation is (x2, + 1e-7); loss within LOSS_TOL.
+    (The C0 gradient goes through 1 / ||T||: fp32 errors there are larger than the dense configs'.)"""
     N, W, D, O = 32768, 256, 129, 2
     gen = torch.Generator(device=DEV).manual_seed(1234)
     X = torch.randn((N, W, D), device=DEV, generator=gen).abs_()
     y = torch.randn((N, O), device=DEV, generator=gen)
-    torch.manual_seed(1)
-    model = CP_linear_regression(X.shape, y.shape, rank_normal=8, rank_spectral=8, n_complex_dim=1, device=DEV)
-    plan = model._get_plan(X, N)
-    assert "slice-1pass-mfma-bf16x3" in plan.describe and "slsp=1" in plan.describe, plan.describe
-    arena = plan.pack(model.Bcp_n, model.Bcp_c, model.bias)
-    w = torch.ones(16, device=DEV)
-    lam = 0.01
-    grad = torch.zeros(plan.num_grads, device=DEV)
-    gtot = torch.zeros(plan.num_params, device=DEV)
-    loss = torch.zeros(1, device=DEV)
-    plan.loss_grad(X, y, None, float(N * O), arena, w, grad)
-    plan.finalize_grad(arena, grad, lam, gtot, loss)
-    data, total, grads, gb = _spectral_fp64(X, y, model.Bcp_n, model.Bcp_c, model.bias, lam)
-    errs = {"data_loss": abs(grad[plan.num_params].item() - data) / abs(data),
-            "loss": abs(loss.item() - total) / abs(total),
-            "bias": normwise_rel(gtot[plan.offsets[6]:].cpu().numpy(), gb.cpu().numpy())}
-    for f, (v, ref) in enumerate(zip(plan.factor_views(gtot), grads)):
-        errs[f"grad{f}"] = normwise_rel(v.cpu().numpy(), ref.cpu().numpy())
-    print("c5", plan.describe, errs)
-    assert errs["data_loss"] <= LOSS_TOL and errs["loss"] <= LOSS_TOL, errs
-    for f in range(6):
-        assert errs[f"grad{f}"] <= GRAD_TOL, errs
-    assert errs["bias"] <= 1e-5, errs
+    d_sp, e_sp = _spectral_errs(X, y, True)
+    d_32, e_32 = _spectral_errs(X, y, False)
+    e_ref = _spectral_ref32_errs(X, y)
+    print("c5 split", d_sp, e_sp)
+    print("c5 f32  ", d_32, e_32)
+    print("c5 ref32", e_ref)
+    assert "slice-1pass-mfma-bf16split" in d_sp and "slsp=1 xpieces=2" in d_sp, d_sp
+    assert "slice-1pass-mfma " in d_32 + " " and "bf16split" not in d_32, d_32
+    for e in (e_sp, e_32):
+        assert e["data_loss"] <= LOSS_TOL and e["loss"] <= LOSS_TOL, e
+        assert e["bias"] <= 1e-5, e
+        for f in range(6):
+            k = f"grad{f}"
+            assert e[k] <= 2 * e_ref[k] + 1e-7, (k, e, e_ref)

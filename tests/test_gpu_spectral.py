@@ -24,11 +24,16 @@ from golden_util import load_spectral, names, normwise_rel
 def spec_path(kind):
     """'fused': the plan's own choice (the single-pass kernel inside its envelope); 'generic':
     force the three-kernel path (TR_SPEC_GENERIC=1, read at plan creation); 'slicef32': the
-    column-slice kernel's f32-MFMA form instead of its default bf16x3 split (TR_SLICE_SPLIT=0)."""
+    column-slice kernel's f32-MFMA form instead of its default bf16 split (TR_SLICE_SPLIT=0);
+    'slicex3': the split form with the sample data in three pieces (TR_SLICE_XPIECES=3) instead of
+    the default two."""
     from tensor_regression_amd import spectral_tensor_regression as SP
     old = os.environ.pop("TR_SPEC_GENERIC", None)
     old_sl = os.environ.pop("TR_SPEC_SLICE", None)
     old_sp = os.environ.pop("TR_SLICE_SPLIT", None)
+    old_xp = os.environ.pop("TR_SLICE_XPIECES", None)
+    if kind == "slicex3":
+        os.environ["TR_SLICE_XPIECES"] = "3"
     if kind == "generic":
         os.environ["TR_SPEC_GENERIC"] = "1"
     if kind == "lockstep":  # the whole-sample lock-step kernel where the column-slice one would run
@@ -42,8 +47,11 @@ def spec_path(kind):
         os.environ.pop("TR_SPEC_GENERIC", None)
         os.environ.pop("TR_SPEC_SLICE", None)
         os.environ.pop("TR_SLICE_SPLIT", None)
+        os.environ.pop("TR_SLICE_XPIECES", None)
         if old_sp is not None:
             os.environ["TR_SLICE_SPLIT"] = old_sp
+        if old_xp is not None:
+            os.environ["TR_SLICE_XPIECES"] = old_xp
         if old is not None:
             os.environ["TR_SPEC_GENERIC"] = old
         if old_sl is not None:
@@ -100,11 +108,11 @@ def test_spectral_golden(name, kind):
         _spectral_golden(name, kind)
 
 
-@pytest.mark.parametrize("kind", ["lockstep", "slicef32"])
+@pytest.mark.parametrize("kind", ["lockstep", "slicef32", "slicex3"])
 @pytest.mark.parametrize("name", [n for n in SPEC if n.startswith("spec_slice")])
 def test_spectral_slice_golden_lockstep(name, kind):
-    """the config-5-shaped fixtures through the whole-sample lock-step kernel and through the
-    column-slice kernel's f32-MFMA form as well"""
+    """the config-5-shaped fixtures through the whole-sample lock-step kernel, the column-slice
+    kernel's f32-MFMA form and its three-piece-X split form as well"""
     with spec_path(kind):
         _spectral_golden(name, kind)
 
@@ -120,11 +128,12 @@ def _spectral_golden(name, kind):
     if name.startswith("spec_slice"):
         # fixtures at config 5's sample shape (W = 256, D = 129 / 100) pin the kernel config 5
         # trains with (k_spec_slice) to the reference's own fit_Adam trajectory
-        assert ("slice-1pass" in desc) == (kind in ("fused", "slicef32")), desc
-        # the default form runs its GEMMs through the exact bf16x3 split
-        assert ("bf16x3" in desc) == (kind == "fused"), desc
-        if kind == "fused":  # lin columns packed (Rn <= 8) or unpacked (spec_slice_rn12_f32x)
-            assert f"slsp={1 if m['rank_normal'] <= 8 else 2}" in desc, desc
+        assert ("slice-1pass" in desc) == (kind in ("fused", "slicef32", "slicex3")), desc
+        # the default form runs its GEMMs through the bf16 split, the sample data in two pieces
+        assert ("bf16split" in desc) == (kind in ("fused", "slicex3")), desc
+        if kind in ("fused", "slicex3"):  # lin columns packed (Rn <= 8) or unpacked (spec_slice_rn12_f32x)
+            sp = (1 if m['rank_normal'] <= 8 else 2) + (2 if kind == "slicex3" else 0)
+            assert f"slsp={sp} xpieces={3 if kind == 'slicex3' else 2}" in desc, desc
     # predict() = lin_model + spectral_model (spectral…py:959-960)
     _close(model.predict(X).numpy(), d["predict0"])
     # one forward + loss + gradient (fit model, spectral…py:716-720)
@@ -269,11 +278,11 @@ def _slice_shape(W, D, Rn, Rs, ncd, O):
     return ok and (38144 + ((small + 3) & ~3) + 4) * 4 <= 160 * 1024
 
 
-@pytest.mark.parametrize("kind", ["lockstep", "slicef32"])
+@pytest.mark.parametrize("kind", ["lockstep", "slicef32", "slicex3"])
 @pytest.mark.parametrize("N,W,D,O,Rn,Rs,ncd,nn", [SHAPES[0]] + SLICE_SHAPES)
 def test_spectral_slice_shapes_lockstep_kernel(N, W, D, O, Rn, Rs, ncd, nn, kind):
-    """the same shapes through the whole-sample lock-step kernel (TR_SPEC_SLICE=0) and the
-    column-slice kernel's f32-MFMA form (TR_SLICE_SPLIT=0)"""
+    """the same shapes through the whole-sample lock-step kernel (TR_SPEC_SLICE=0), the
+    column-slice kernel's f32-MFMA form (TR_SLICE_SPLIT=0) and its three-piece-X split form"""
     with spec_path(kind):
         _spectral_shape(N, W, D, O, Rn, Rs, ncd, nn, kind)
 
@@ -308,10 +317,11 @@ def _spectral_shape(N, W, D, O, Rn, Rs, ncd, nn, kind):
     if kind == "generic" or (kind == "fused" and wide):
         assert "generic" in plan.describe, plan.describe
     slice_ok = _slice_shape(W, D, Rn, Rs, ncd, O)
-    assert ("slice" in plan.describe) == (kind in ("fused", "slicef32") and slice_ok), plan.describe
-    assert ("bf16x3" in plan.describe) == (kind == "fused" and slice_ok), plan.describe
-    if kind == "fused" and slice_ok:  # lin columns packed two split parts per tile (Rn <= 8) or not
-        assert f"slsp={1 if Rn <= 8 else 2}" in plan.describe, plan.describe
+    assert ("slice" in plan.describe) == (kind in ("fused", "slicef32", "slicex3") and slice_ok), plan.describe
+    assert ("bf16split" in plan.describe) == (kind in ("fused", "slicex3") and slice_ok), plan.describe
+    if kind in ("fused", "slicex3") and slice_ok:  # lin columns packed two split parts per tile (Rn <= 8) or not
+        sp = (1 if Rn <= 8 else 2) + (2 if kind == "slicex3" else 0)
+        assert f"slsp={sp} xpieces={3 if kind == 'slicex3' else 2}" in plan.describe, plan.describe
     arena = plan.pack(model.Bcp_n, model.Bcp_c, model.bias)
     w = torch.ones(Rn + Rs, device=DEV)
     grad = torch.zeros(plan.num_grads, device=DEV)

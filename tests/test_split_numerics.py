@@ -1,17 +1,50 @@
 """Numerics of the exact three-term bf16 split the column-slice spectral kernel runs its GEMMs
 with (csrc/tr_spectral_slice.hip: sl_split2 / sl_mfma6 / sl_mfma_lp), restated in numpy on the
-fp32 bit patterns (CPU; the kernel itself is covered by tests/test_gpu_spectral.py).
+fp32 bit patterns (CPU; the kernel itself is covered by tests/test_gpu_spectral.py and, at full
+config-5 size against fp64, tests/test_gpu_fullsize.py).
 
-  x1 = x with the low 16 bits cleared (top 8 significand bits), r = x - x1 (exact),
-  x2 = r with the low 16 bits cleared, x3 = r - x2 (at most 8 significant bits: a bf16)
-  a.b ~ a1b1 + a1b2 + a2b1 + a1b3 + a2b2 + a3b1   (dropped: a2b3 + a3b2 + a3b3 < 2^-20 |ab|)
+  x1 = bf16_rne(x), r = x - x1 (exact), x2 = bf16_rne(r), x3 = r - x2 (at most 8 significant
+  bits: exactly a bf16)  (TR_SLICE_SPLITMODE 2, the default)
+  a.b ~ a1b1 + a1b2 + a2b1 + a1b3 + a2b2 + a3b1   (dropped: a2b3 + a3b2 + a3b3 < 2^-24 |ab|)
+
+The round-3 split truncated every piece (split3_trunc below, TR_SLICE_SPLITMODE 0): its pieces
+all carry the sign of x, so the dropped terms are biased toward the sign of ab, and over the
+config-5 gradient sums that bias came to 8-25x the f32 MFMA form's error.  Mode 1 truncates x1
+and rounds x2 / x3 (unbiased, dropped terms < 2^-22 |ab|).
 """
 import numpy as np
+import pytest
 
 MASK = np.uint32(0xFFFF0000)
 
 
+def rne_bf16(v):
+    """fp32 -> bf16 (round to nearest even) -> fp32, as v_cvt_pk_bf16_f32 (finite inputs)"""
+    u = np.asarray(v, dtype=np.float32).view(np.uint32).astype(np.uint64)
+    return (((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16).astype(np.uint32).view(np.float32)
+
+
 def split3(x):
+    """TR_SLICE_SPLITMODE 2 (default): every piece by round-to-nearest"""
+    x = np.asarray(x, dtype=np.float32)
+    x1 = rne_bf16(x)
+    r = (x - x1).astype(np.float32)
+    x2 = rne_bf16(r)
+    x3 = (r - x2).astype(np.float32)
+    return x1, x2, x3
+
+
+def split3_hybrid(x):
+    """TR_SLICE_SPLITMODE 1: x1 truncated, x2 by round-to-nearest"""
+    x = np.asarray(x, dtype=np.float32)
+    x1 = (x.view(np.uint32) & MASK).view(np.float32)
+    r = (x - x1).astype(np.float32)
+    x2 = rne_bf16(r)
+    return x1, x2, (r - x2).astype(np.float32)
+
+
+def split3_trunc(x):
+    """TR_SLICE_SPLITMODE 0 (round 3): every piece truncated"""
     x = np.asarray(x, dtype=np.float32)
     x1 = (x.view(np.uint32) & MASK).view(np.float32)
     r = (x - x1).astype(np.float32)
@@ -26,12 +59,15 @@ def _rand(n, seed):
     x = (g.standard_normal(n) * np.exp2(g.integers(-60, 60, n))).astype(np.float32)
     x[:8] = np.array([1.0, -1.0, 3.0000002, np.float32(1) - np.float32(2 ** -24), 1e-30, -7.5e30,
                       np.float32(0.1), 0.0], dtype=np.float32)
-    return x
+    # the kernel's domain: finite, below the bf16 overflow threshold (3.39e38)
+    return x[np.isfinite(x) & (np.abs(x) < 3.3e38)]
 
 
-def test_split_is_exact_and_bf16():
+@pytest.mark.parametrize("mode", [2, 1, 0])
+def test_split_is_exact_and_bf16(mode):
+    sp = {2: split3, 1: split3_hybrid, 0: split3_trunc}[mode]
     x = _rand(200000, 0)
-    x1, x2, x3 = split3(x)
+    x1, x2, x3 = sp(x)
     # every piece is a bf16 (low 16 bits zero) and the pieces sum back to x exactly
     for p in (x1, x2, x3):
         assert not np.any(p.view(np.uint32) & np.uint32(0xFFFF))
@@ -39,22 +75,63 @@ def test_split_is_exact_and_bf16():
     assert np.array_equal(s, x.astype(np.float64))
     # magnitude bounds the error analysis uses
     ax = np.abs(x.astype(np.float64))
-    assert np.all(np.abs(x2) <= ax * 2.0 ** -7)
-    assert np.all(np.abs(x3) <= ax * 2.0 ** -14)
+    b2, b3 = {2: (-8, -17), 1: (-7, -16), 0: (-7, -14)}[mode]
+    assert np.all(np.abs(x2) <= ax * 2.0 ** b2)
+    assert np.all(np.abs(x3) <= ax * 2.0 ** b3)
 
 
-def test_six_term_product_error():
-    a, b = _rand(100000, 1), _rand(100000, 2)
-    a1, a2, a3 = (p.astype(np.float64) for p in split3(a))
-    b1, b2, b3 = (p.astype(np.float64) for p in split3(b))
+def _six_term_rel(sp, seed_a=1, seed_b=2, n=200000):
+    a, b = _rand(n, seed_a), _rand(n, seed_b)
+    m = min(len(a), len(b))
+    a, b = a[:m], b[:m]
+    a1, a2, a3 = (p.astype(np.float64) for p in sp(a))
+    b1, b2, b3 = (p.astype(np.float64) for p in sp(b))
     six = a1 * b1 + a1 * b2 + a2 * b1 + a1 * b3 + a2 * b2 + a3 * b1
     exact = a.astype(np.float64) * b.astype(np.float64)
     nz = exact != 0
-    rel = np.abs(six[nz] - exact[nz]) / np.abs(exact[nz])
-    # the bound the kernel comment, the public header and DESIGN.md state: < 2^-20 |ab| worst case
-    # (measured 2^-21.3 on this kind of sample), typically 2^-25 (below the fp32 product rounding)
-    assert rel.max() < 2.0 ** -20
-    assert np.median(rel) < 2.0 ** -24
+    return (six[nz] - exact[nz]) / np.abs(exact[nz]), np.sign(exact[nz])
+
+
+def test_six_term_product_error():
+    # the bound the kernel comment, the public header and DESIGN.md state for the default split:
+    # < 2^-24 |ab| worst case (measured 2^-24.3), median 2^-29; no bias toward the sign of ab
+    rel, sgn = _six_term_rel(split3)
+    assert np.abs(rel).max() < 2.0 ** -24
+    assert np.median(np.abs(rel)) < 2.0 ** -28
+    assert abs((rel * sgn).mean()) < 0.01 * 2.0 ** -24
+    rel, sgn = _six_term_rel(split3_hybrid)
+    assert np.abs(rel).max() < 2.0 ** -22
+    assert abs((rel * sgn).mean()) < 0.01 * 2.0 ** -24
+
+
+def test_truncating_split_is_biased():
+    """the round-3 split: the dropped terms pull every product toward zero (relative -0.69 x 2^-24
+    on average), which is what summed to the full-size gradient error the default avoids"""
+    rel, sgn = _six_term_rel(split3_trunc)
+    assert np.abs(rel).max() < 2.0 ** -20
+    assert (rel * sgn).mean() < -0.3 * 2.0 ** -24
+
+
+def test_biased_split_error_grows_with_cancellation():
+    """a long signed sum with heavy cancellation (a gradient over many samples): the unbiased
+    split stays at the fp32 accumulation's error level, the truncating one does not"""
+    g = np.random.default_rng(7)
+    n = 1 << 18
+    a = np.abs(g.standard_normal(n)).astype(np.float32)
+    b = (g.standard_normal(n) * 0.2).astype(np.float32)
+    b -= np.float32(np.dot(a.astype(np.float64), b.astype(np.float64)) / np.dot(a.astype(np.float64), a))
+    b = b.astype(np.float32) * np.float32(1) + np.float32(1e-3)  # small mean: strong cancellation
+    exact = float(np.dot(a.astype(np.float64), b.astype(np.float64)))
+    scale = float(np.abs(a.astype(np.float64) * b.astype(np.float64)).sum())
+
+    def six(sp):
+        a1, a2, a3 = (p.astype(np.float64) for p in sp(a))
+        b1, b2, b3 = (p.astype(np.float64) for p in sp(b))
+        return float((a1 * b1 + a1 * b2 + a2 * b1 + a1 * b3 + a2 * b2 + a3 * b1).sum())
+    e_rne = abs(six(split3) - exact) / scale
+    e_trunc = abs(six(split3_trunc) - exact) / scale
+    assert e_rne < 2.0 ** -30
+    assert e_trunc > 8 * e_rne
 
 
 def test_packed_lin_columns_sum_to_the_six_terms():

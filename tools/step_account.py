@@ -45,22 +45,13 @@ def main():
     dom = [i for i, r in enumerate(rows) if args.dominant in r[2]]
     if len(dom) < K + 1:
         raise SystemExit(f"{len(dom)} launches of {args.dominant}, need {K + 1}")
-    # first timed iteration starts right after the last kernel of the iteration before it: the
-    # kernels between the (K+1)-th-last and the K-th-last dominant launch form one iteration
+    # the timed fit is the last one in the trace: it ends with the last kernel, and it starts with
+    # the first kernel after the largest idle gap between the (K+1)-th-last dominant launch (the
+    # warm-up fit's last iteration) and the K-th-last one (the host's fit set-up lies in that gap)
     prev, first = dom[-K - 1], dom[-K]
-    per_iter = first - prev
-    start_idx = first - (per_iter - 1) if per_iter > 1 else first
-    # the iteration's first kernel is the one after the previous iteration's last: find the
-    # dominant kernel's offset inside an iteration from the run's kernel sequence
-    seq = [r[2] for r in rows[prev:first]]
-    k_off = 0  # kernels of an iteration launched before the dominant one
-    names_after = seq[1:]
-    # kernels launched before the dominant one in an iteration = those after it in the cycle
-    # that belong to the next iteration: the prep kernel(s) named in bench's launch list
-    pre = [n for n in names_after if "build_dense" in n or "prep" in n]
-    k_off = len(pre)
-    start_idx = first - k_off
-    end_idx = dom[-1] + (per_iter - 1 - k_off)
+    gaps_b = [(rows[i + 1][0] - rows[i][1], i + 1) for i in range(prev, first)]
+    start_idx = max(gaps_b)[1]
+    end_idx = len(rows) - 1
     win = rows[start_idx:end_idx + 1]
     t0, t1 = win[0][0], win[-1][1]
     busy = defaultdict(int)
@@ -71,7 +62,7 @@ def main():
     gaps = 0
     for a, b in zip(win, win[1:]):
         gaps += max(0, b[0] - a[1])
-    out = {"steps": K, "kernels_per_step": per_iter, "gpu_window_ms_per_step": (t1 - t0) / 1e6 / K,
+    out = {"steps": K, "kernels_in_window": len(win), "gpu_window_ms_per_step": (t1 - t0) / 1e6 / K,
            "kernel_ms_per_step": {n: busy[n] / 1e6 / K for n in busy},
            "kernel_mean_us": {n: busy[n] / 1e3 / count[n] for n in busy},
            "kernels_sum_ms_per_step": sum(busy.values()) / 1e6 / K, "gaps_ms_per_step": gaps / 1e6 / K}
