@@ -526,7 +526,7 @@ def main():
         if "bf16split" in plan.describe:
             # fp32 operands and accumulation; the GEMMs run on the bf16 matrix cores through split
             # operands (DESIGN.md "bf16 split GEMMs"): factors / dT in three round-to-nearest pieces
-            # (exact), the sample data in two (|x - x1 - x2| <= 2^-17 |x|) or three
+            # (exact), the sample data in two (|x - x1 - x2| < 2^-16 |x|) or three
             xp = "three" if "xpieces=3" in plan.describe else "two"
             out["roofline"]["gemm_form"] = (f"bf16 split GEMMs: factor-side operands in three RNE bf16 pieces, X in "
                                             f"{xp}, fp32 accumulate")

@@ -253,7 +253,7 @@ int tr_adam_step_f64(tr_plan* plan, double* params, const double* grad, double* 
  *                      described as slice-1pass-mfma-bf16split when its GEMMs run on the bf16
  *                      matrix cores through split operands (the default): factor-side operands in
  *                      three round-to-nearest bf16 pieces (exact), the sample data in two
- *                      (|x - x1 - x2| <= 2^-17 |x|, unbiased), fp32 accumulation.  At full config-5
+ *                      (|x - x1 - x2| < 2^-16 |x|, measured 2^-17, unbiased), fp32 accumulation.  At full config-5
  *                      size its gradients lie within 3.5e-7 normwise of an fp64 closed form (the
  *                      f32 MFMA form 1.1e-7, the reference's own fp32 op sequence 0.6-4.2e-6);
  *                      results are not bitwise those of the f32 MFMA form.  Environment, read at
