@@ -11,6 +11,10 @@ The round-3 split truncated every piece (split3_trunc below, TR_SLICE_SPLITMODE 
 all carry the sign of x, so the dropped terms are biased toward the sign of ab, and over the
 config-5 gradient sums that bias came to 8-25x the f32 MFMA form's error.  Mode 1 truncates x1
 and rounds x2 / x3 (unbiased, dropped terms < 2^-22 |ab|).
+
+By default the kernel splits only the factor side (Phi0, dT) in three; the sample data X goes in
+two round-to-nearest pieces (split2_rne, |x - x1 - x2| < 2^-16 |x|), five MFMAs per product
+instead of six.  TR_SLICE_XPIECES=3 splits X in three as well (the six terms above).
 """
 import numpy as np
 import pytest
@@ -170,7 +174,8 @@ def test_dot_product_matches_fp32_quality():
 
 
 def split2_rne(x):
-    """TR_SLICE_X2 (off by default): the X side as two round-to-nearest-even bf16 pieces"""
+    """the sample side (X) as two round-to-nearest-even bf16 pieces: the default
+    (TR_SLICE_XPIECES=3 selects split3 for X as well)"""
     x = np.asarray(x, dtype=np.float32)
 
     def rne_bf16(v):
