@@ -69,6 +69,19 @@ CONFIGS["c7"] = dict(kind="linear", rows=65536, dims=(256, 128), rank=8, hoststr
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32 = the fp32 vector rate
 
 
+class _Phases:
+    """TR_BENCH_PHASES=1: host time of each set-up phase around the timed fit, on stderr"""
+    def __init__(self):
+        self.on = os.environ.get("TR_BENCH_PHASES") == "1"
+        self.t = time.perf_counter()
+
+    def __call__(self, what):
+        if self.on:
+            now = time.perf_counter()
+            log(f"bench phase {what}: {1e3 * (now - self.t):.3f} ms")
+            self.t = now
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -378,7 +391,9 @@ def main():
             return model.fit_Adam(lambda_L2=0.01, max_iter=iters, tol=0, patience=10, weights=cw,
                                   Adam_kwargs={"lr": 0.01}, process_group=pg)
 
+    _ph = _Phases()
     fit(args.warmup)
+    _ph("warm-up fit")
     plan = model._plan
     # the kernel strategy this config is benchmarked on: a silent fallback (e.g. a spilling
     # single-pass variant dropping the plan to two passes) must not pass as this config's number
@@ -386,7 +401,9 @@ def main():
     if want and (f"path={want}" not in plan.describe or "recovered=" in plan.describe) and not args.allow_other_path:
         raise SystemExit(f"bench {args.config}: plan took an unexpected path ({plan.describe}); expected "
                          f"path={want} (--allow-other-path to measure it anyway)")
+    _ph("plan path check")
     plan.read_timing()
+    _ph("read_timing")
     # time only the X-streaming kernels by default (timing-only events, no system-scope fence:
     # with the default fence each record idled the GPU ~6 us on its side of the launch in a
     # rocprofv3 kernel trace; --timing-every n brackets only every n-th launch)
@@ -398,8 +415,10 @@ def main():
         if pg is not None:
             torch.distributed.barrier()
 
+    _ph("set_timing")
     barrier()
     torch.cuda.synchronize()
+    _ph("barrier + sync")
     t0 = time.perf_counter()
     fit(args.steps)
     torch.cuda.synchronize()
