@@ -74,6 +74,11 @@
 #define TR_SLICE_BKW 4  // wave that keeps the per-sample bookkeeping (dA2 / dC2 / bias / loss / y_hat,
                         // tail-row sums): a second-half wave, off the first half's critical path
 #endif
+#ifndef TR_SLICE_TAILLAST
+#define TR_SLICE_TAILLAST 1  // split kernels: the tail column's dword LDS-DMA goes out after the sample's
+                             // 16 tile pieces (its 128-B lines are then already on their way into L2)
+                             // instead of before them (0: every tail dword was its own HBM sector miss)
+#endif
 #ifndef TR_SLICE_NOSEL
 #define TR_SLICE_NOSEL 1  // epilogue table reads without per-element lane masks (see tab8)
 #endif
@@ -492,10 +497,15 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
       sl_dma4(X + n * xld + w * D + 128 + tr, sTail);
     }
   };
-  auto dma_sample = [&](int64_t n) {  // tail first: waiting for tile 0 also retires it
-    if (Dt > 0) dma_tail(n);
+  // split kernels (TR_SLICE_TAILLAST): the tail goes last, after every tile piece of the sample;
+  // otherwise first (waiting for tile 0 also retires it: the f32 form reads it inside the loop)
+  constexpr bool TAIL_LAST = SP && TR_SLICE_TAILLAST;
+  constexpr int NTL = (TAIL_LAST && Dt > 0) ? 1 : 0;  // tail pieces issued after the tiles
+  auto dma_sample = [&](int64_t n) {
+    if (Dt > 0 && !TAIL_LAST) dma_tail(n);
 #pragma unroll
     for (int q = 0; q < SL_TILES; ++q) dma_tile(n, q);
+    if (Dt > 0 && TAIL_LAST) dma_tail(n);
   };
 
   __builtin_amdgcn_s_waitcnt(0);  // retire the prologue's loads (the loop's waits are counted)
@@ -552,7 +562,7 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
       }
       {
         SL_SUB_BEGIN();
-        sl_wait_vm((ntl - 1) * 2 + npf);
+        sl_wait_vm((ntl - 1) * 2 + NTL + npf);
         SL_SUB_END(1);
       }
 #pragma unroll
@@ -562,7 +572,7 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
         if (q + 1 < ntl) {
           {
             SL_SUB_BEGIN();
-            sl_wait_vm((ntl - 2 - q) * 2 + npf);
+            sl_wait_vm((ntl - 2 - q) * 2 + NTL + npf);
             SL_SUB_END(1);
           }
 #pragma unroll
@@ -641,6 +651,7 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
         // (rows >= Dt zero), element j <-> w offset 4 j + gq of the wave's 32 tail w (after the
         // loop: nothing of the forward is live; one case per static S)
         sl_u4 tf[3];
+        if (NTL) sl_wait_vm(npf);  // the tail (issued after the tiles) has landed
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
           const float x0 = i < Dt ? sTail[i * TR + 8 * m + gq] : 0.f;
@@ -840,7 +851,7 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
         bo0 = bo_of(L, 0);
         bo1 = bo_of(L, 1);
       }
-      if (has_next && Dt > 0) {
+      if (has_next && Dt > 0 && !TAIL_LAST) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         dma_tail(nn);
       }
@@ -930,6 +941,8 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
           }
         }
       }
+      // (this wave's tail operands were read at the top of the phase, and its tile reads waited)
+      if (TAIL_LAST && has_next && Dt > 0) dma_tail(nn);
     }
     SL_MARK(7);
   }
