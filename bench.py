@@ -392,7 +392,17 @@ def main():
                                   Adam_kwargs={"lr": 0.01}, process_group=pg)
 
     _ph = _Phases()
-    fit(args.warmup)
+    if _ph.on:  # where the warm-up (first) fit call spends its host time
+        import cProfile
+        import pstats
+        prof = cProfile.Profile()
+        prof.enable()
+        fit(args.warmup)
+        prof.disable()
+        pstats.Stats(prof, stream=sys.stderr).sort_stats("cumulative").print_stats(35)
+        pstats.Stats(prof, stream=sys.stderr).sort_stats("tottime").print_stats(15)
+    else:
+        fit(args.warmup)
     _ph("warm-up fit")
     plan = model._plan
     # the kernel strategy this config is benchmarked on: a silent fallback (e.g. a spilling
