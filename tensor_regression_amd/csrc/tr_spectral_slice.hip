@@ -274,6 +274,17 @@ __device__ __forceinline__ void sl_barrier() {
 __device__ __forceinline__ uint32_t sl_lds_addr(const float* p) {
   return (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) float*)p);
 }
+// sl_dma16b with soffset = tstr * q and the LDS address lds_b + lds_off formed by the statement
+// itself from a base and constants (formed outside, the compiler hoisted all sixteen out of the
+// sample loop into SGPRs the kernel does not have: one spill reload per piece)
+__device__ __forceinline__ void sl_dma16bq(__amdgpu_buffer_rsrc_t rs, uint32_t tstr, uint32_t q, uint32_t voff,
+                                           uint32_t lds_b, uint32_t lds_off) {
+  uint32_t keep, so;
+  asm volatile("s_mul_i32 %1, %4, %5\n\ts_mov_b32 %0, m0\n\ts_add_u32 m0, %3, %7\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %6, %1 offen lds" SL_NT "\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep), "=&s"(so)
+               : "v"(voff), "s"(lds_b), "s"(tstr), "s"(q), "s"(rs), "s"(lds_off)
+               : "memory", "scc");
+}
 // one 4-B LDS-DMA piece per lane: gsrc -> LDS byte address m0 + 4 * lane (m0 saved / restored)
 __device__ __forceinline__ void sl_dma4(const float* gsrc, const float* lds_dst) {
   uint32_t keep;
@@ -292,11 +303,13 @@ __device__ __forceinline__ void sl_dma16(const float* gsrc, const float* lds_dst
 }
 // one 16-B LDS-DMA piece per lane through a buffer descriptor: rsrc base + soff + voff (lane) -> LDS
 // byte address m0 + 16 * lane; no per-lane 64-bit address arithmetic at the call
-__device__ __forceinline__ void sl_dma16b(__amdgpu_buffer_rsrc_t rs, uint32_t soff, uint32_t voff, const float* lds_dst) {
+// (lds_b: the destination's LDS byte address, wave-uniform: formed from a 32-bit base and a
+// compile-time offset, no generic-pointer cast with its null check at every piece)
+__device__ __forceinline__ void sl_dma16b(__amdgpu_buffer_rsrc_t rs, uint32_t soff, uint32_t voff, uint32_t lds_b) {
   uint32_t keep;
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds" SL_NT "\n\ts_mov_b32 m0, %0"
                : "=&s"(keep)
-               : "v"(voff), "s"(rs), "s"(__builtin_amdgcn_readfirstlane(sl_lds_addr(lds_dst))), "s"(soff)
+               : "v"(voff), "s"(rs), "s"(lds_b), "s"(soff)
                : "memory");
 }
 // s_waitcnt vmcnt(n), n wave-uniform in [0, 63]
@@ -355,6 +368,7 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
   const bool vlane = rs_ok && (i % CC) == 0;  // lane that carries V / dPhi(C1) of rank rs
 
   float* slice = lds + wv * SL_SLICE;
+  const uint32_t slice_b = (uint32_t)__builtin_amdgcn_readfirstlane(sl_lds_addr(slice));  // its LDS byte address
   float* sTail = lds + SL_O_TAIL + wv * SL_TAIL;  // [Dt][TR]
   float* sEx = lds + SL_O_EX;                      // [8 waves][64 lanes][8]
   float* sTP = lds + SL_O_TP;                      // [8 waves][2 rows][32 columns]
@@ -474,15 +488,18 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
     dvo[0] = dvo_of(L, 0);
     dvo[1] = dvo_of(L, 1);
   };
-  const uint32_t sbytes = (uint32_t)(g.W * D * 4);
+  // the descriptor starts at this wave's half of the sample (row wbase); tile q's rows are at
+  // soffset q * tstr, formed inside the piece's statement (hoisted out of the sample loop, the
+  // eight tile offsets took SGPRs the kernel does not have: one spill reload per piece)
+  const uint32_t hbytes = (uint32_t)((g.W - wbase) * D * 4), tstr = (uint32_t)(64 * D);
   auto rsrc_of = [&](int64_t n) {
-    const uint64_t a = (uint64_t)(uintptr_t)(X + n * xld);
+    const uint64_t a = (uint64_t)(uintptr_t)(X + n * xld + (int64_t)wbase * D);
     const uint64_t au = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(a >> 32)) << 32) |
                         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a);
-    return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)au, (short)0, (int)sbytes, 0x00020000);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)au, (short)0, (int)hbytes, 0x00020000);
   };
   auto dma_piece_r = [&](__amdgpu_buffer_rsrc_t rs, int q, int c4) {  // chunks 8q + 4c4 .. +3
-    sl_dma16b(rs, (uint32_t)((wbase + 16 * q) * D * 4), dvo[c4], slice + 64 * (8 * q + 4 * c4));
+    sl_dma16bq(rs, tstr, (uint32_t)q, dvo[c4], slice_b, 256u * (uint32_t)(8 * q + 4 * c4));
   };
   auto dma_piece = [&](int64_t n, int q, int c4) { dma_piece_r(rsrc_of(n), q, c4); };
   auto dma_tile = [&](int64_t n, int q) {
@@ -952,6 +969,11 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
     for (int q = 0; q < 8; ++q) g_slice_prof[blockIdx.x][wv][q] = prof[q];
 #endif
   // ---- per-workgroup slab (arena layout, phi space) -------------------------------------------
+  // lane-dependent indices formed afresh from an opaque lane index (held across the sample loop
+  // from the prologue, two of them were spilled to scratch: the launch then needed scratch memory)
+  const int lp = sl_lane_now();
+  const int tp = wv * TR_WAVE + lp, ip = lp & 15, gqp = lp >> 4, rsp = ip / CC;
+  const bool vlp = rsp < Rs && (ip % CC) == 0;
   __syncthreads();  // (no LDS-DMA in flight: the last sample issued none)
   if constexpr (SL_LP(SP)) {  // packed lin columns
 #pragma unroll
@@ -962,13 +984,13 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
 #pragma unroll
   for (int q = 0; q < SL_TILES; ++q)
 #pragma unroll
-    for (int jt = 0; jt < 2; ++jt) *reinterpret_cast<sl_f4*>(slice + ((q * 2 + jt) * TR_WAVE + lane) * 4) = gacc[q][jt];
-  *reinterpret_cast<sl_f4*>(sEx + (wv * TR_WAVE + lane) * 8) = sl_f4{an1[0][0], an1[0][1], an1[0][2], an1[0][3]};
-  *reinterpret_cast<sl_f4*>(sEx + (wv * TR_WAVE + lane) * 8 + 4) = sl_f4{an1[1][0], an1[1][1], an1[1][2], an1[1][3]};
+    for (int jt = 0; jt < 2; ++jt) *reinterpret_cast<sl_f4*>(slice + ((q * 2 + jt) * TR_WAVE + lp) * 4) = gacc[q][jt];
+  *reinterpret_cast<sl_f4*>(sEx + (wv * TR_WAVE + lp) * 8) = sl_f4{an1[0][0], an1[0][1], an1[0][2], an1[0][3]};
+  *reinterpret_cast<sl_f4*>(sEx + (wv * TR_WAVE + lp) * 8 + 4) = sl_f4{an1[1][0], an1[1][1], an1[1][2], an1[1][3]};
   __syncthreads();
   float* sl = slab + (int64_t)blockIdx.x * slab_stride;
   // dPhi0 (A0 and C0 columns): the four pairs' partials in pair order
-  for (int e = t; e < g.W * 32; e += SL_T) {
+  for (int e = tp; e < g.W * 32; e += SL_T) {
     const int w = e >> 5, jc = e & 31;
     const int h2 = w / WH, wl = w - h2 * WH;
     const int q = wl >> 4, gg = (wl & 15) >> 2, reg = wl & 3, jt = jc >> 4, ii = jc & 15;
@@ -984,27 +1006,27 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
   }
   // dPhi(A1) rows d < 128: the two halves' partials; dPhi(C1): the owner lane's own sum
   const int Dm = D < 128 ? D : 128;
-  for (int e = t; e < Dm * Rn; e += SL_T) {
+  for (int e = tp; e < Dm * Rn; e += SL_T) {
     const int d = e / Rn, r = e - d * Rn;
     const int p2 = d >> 5, c = d & 31, gg = c >> 3, v = (c & 7) >> 1, h = c & 1;
     const int li = 16 * gg + r;
     sl[g.offA1 + e] = sEx[(p2 * TR_WAVE + li) * 8 + 4 * h + v] + sEx[((p2 + 4) * TR_WAVE + li) * 8 + 4 * h + v];
   }
-  if (vlane) {
+  if (vlp) {
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
-      const int d = dbase + 8 * gq + 2 * v + hw;
-      if (d < D) sl[g.offC1 + (int64_t)d * Rs + rs] = as1[v];
+      const int d = dbase + 8 * gqp + 2 * v + hw;
+      if (d < D) sl[g.offC1 + (int64_t)d * Rs + rsp] = as1[v];
     }
   }
-  if (wv == 0 && Dt > 0 && gq < Dt) {
-    if (i < Rn) sl[g.offA1 + (int64_t)(128 + gq) * Rn + i] = sTacc[gq * 32 + i];
-    if (vlane) sl[g.offC1 + (int64_t)(128 + gq) * Rs + rs] = sTacc[gq * 32 + 16 + rs];
+  if (wv == 0 && Dt > 0 && gqp < Dt) {
+    if (ip < Rn) sl[g.offA1 + (int64_t)(128 + gqp) * Rn + ip] = sTacc[gqp * 32 + ip];
+    if (vlp) sl[g.offC1 + (int64_t)(128 + gqp) * Rs + rsp] = sTacc[gqp * 32 + 16 + rsp];
   }
-  for (int e = t; e < NO * Rn; e += SL_T) sl[g.offA2 + e] = sAcc[e];
-  for (int e = t; e < NO * Rs; e += SL_T) sl[g.offC2 + e] = sAcc[NO * Rn + e];
-  for (int e = t; e < NO; e += SL_T) sl[g.offB + e] = sAcc[NO * (Rn + Rs) + e];
-  if (t == 0) {
+  for (int e = tp; e < NO * Rn; e += SL_T) sl[g.offA2 + e] = sAcc[e];
+  for (int e = tp; e < NO * Rs; e += SL_T) sl[g.offC2 + e] = sAcc[NO * Rn + e];
+  for (int e = tp; e < NO; e += SL_T) sl[g.offB + e] = sAcc[NO * (Rn + Rs) + e];
+  if (tp == 0) {
     dpart[2 * blockIdx.x] = *sLoss;
     dpart[2 * blockIdx.x + 1] = 0.0;
   }
