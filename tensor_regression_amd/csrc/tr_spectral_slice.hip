@@ -133,18 +133,23 @@ __device__ __forceinline__ sl_f4 sl_mfma(float a, float b, sl_f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-// ---- exact three-term bf16 split (SP > 0) ---------------------------------------------------
+// ---- round-to-nearest bf16 split (SP > 0) --------------------------------------------------
 // x = x1 + x2 + x3 by round-to-nearest-even bf16 conversions (v_cvt_pk_bf16_f32, two values per
 // instruction): x1 = bf16(x), r = x - x1 (exact: Sterbenz), x2 = bf16(r), x3 = r - x2 (exact, at
 // most 8 significant bits: exactly a bf16), for every finite |x| below the bf16 overflow
 // threshold (3.39e38) and above 2^-100.  |x2| <= 2^-8 |x|, |x3| <= 2^-17 |x|, and — unlike a
 // truncating split, whose pieces all carry the sign of x — the pieces' signs are independent of
-// x.  A product a.b is formed as the six cross terms of weight >= 2^-17 (a1b1, a1b2, a2b1, a1b3,
-// a2b2, a3b1) on v_mfma_f32_16x16x32_bf16 (16x the f32 MFMA rate), each exact in the fp32
-// accumulator; the dropped a2b3 + a3b2 + a3b3 weigh < 2^-24 |ab| (measured maximum 2^-24.3,
-// median 2^-29), below the fp32 rounding of the product itself, and have no bias toward the sign
-// of ab (a truncating split's dropped terms do: at config 5 that bias summed to 8-25x the f32
-// MFMA form's gradient error).  tests/test_split_numerics.py holds these bounds.
+// x.  The factor side (Phi0 fragments, dT) is always split in three.  The sample side X is split
+// in two by default (SL_XP(SP) == 2: x1 + x2, |x - x1 - x2| < 2^-16 |x|, measured maximum 2^-17.0,
+// median 2^-19.4, unbiased) and a product x.f is formed as the five cross terms x1f1, x1f2, x2f1,
+// x1f3, x2f2; with TR_SLICE_XPIECES=3 (SP 3, 4) X is split in three as well and the six terms of
+// weight >= 2^-17 are formed (x3f1 added), the dropped x2f3 + x3f2 + x3f3 weighing < 2^-24 |xf|
+// (measured maximum 2^-24.3, median 2^-29).  Every term is an exact bf16 x bf16 product in the
+// fp32 accumulator of v_mfma_f32_16x16x32_bf16 (16x the f32 MFMA rate).  At full config-5 size
+// the default form's gradients lie within 3.5e-7 of fp64 (the reference's own fp32 op sequence:
+// 0.6-4.2e-6; a truncating split's dropped terms are biased toward the sign of the product, and
+// over config 5's sums that bias reached 8-25x the f32 MFMA form's error).
+// tests/test_split_numerics.py holds these bounds, tests/test_gpu_fullsize.py the full-size errors.
 typedef __bf16 sl_bf8 __attribute__((ext_vector_type(8)));
 typedef __bf16 sl_bf2 __attribute__((ext_vector_type(2)));
 typedef uint32_t sl_u4 __attribute__((ext_vector_type(4)));
@@ -339,8 +344,9 @@ __device__ __forceinline__ int sl_lane_now() {
 __device__ __forceinline__ int sl_swz(int x) { return (x & 1) | ((x & 2) << 1); }
 }  // namespace
 
-// SP: 0 = both GEMMs on v_mfma_f32_16x16x4_f32; 1 = exact three-term bf16 split on
-// v_mfma_f32_16x16x32_bf16 with the lin columns packed (Rn <= 8); 2 = split, lin unpacked
+// SP: 0 = both GEMMs on v_mfma_f32_16x16x4_f32; 1 = bf16 split on v_mfma_f32_16x16x32_bf16 (X in
+// two pieces) with the lin columns packed (Rn <= 8); 2 = the same, lin unpacked; 3 / 4 = X in three
+// pieces (TR_SLICE_XPIECES=3), lin packed / unpacked
 template <int CC, int DT, int SP>
 __global__ __launch_bounds__(SL_T) void k_spec_slice(
     const float* __restrict__ X, int64_t N, int64_t xld, SpecGeom g, const float* __restrict__ phi,
