@@ -249,3 +249,12 @@ hipError_t launch_linear_cluster(int CH, int S, int ncl, const float* X, int64_t
 }
 
 }  // namespace tr
+
+namespace tr {
+// this translation unit's code object, loaded when the first plan is created (tr_api.hip:
+// preload_code_objects) instead of at the first launch of one of its kernels
+hipError_t touch_code_object_cluster() {
+  hipFuncAttributes a;
+  return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&k_linear_cluster<15>));
+}
+}  // namespace tr

@@ -101,3 +101,19 @@ __device__ __forceinline__ float4 tr_ld_stream(const float4* p) {
   const tr_f4 v = __builtin_nontemporal_load(reinterpret_cast<const tr_f4*>(p));
   return make_float4(v.x, v.y, v.z, v.w);
 }
+
+// HIP loads every translation unit's code object (one per .hip file of the library) on the first
+// use of any of its kernels: loading tr_kernels.hip's took 10.5 ms inside the first fit's first
+// iteration on the GPU box.  Each file defines one touch function; tr_api.hip calls them all once
+// per device when a plan is created.
+namespace tr {
+hipError_t touch_code_object_kernels();
+hipError_t touch_code_object_update();
+hipError_t touch_code_object_cluster();
+hipError_t touch_code_object_spectral();
+hipError_t touch_code_object_spectral_slice();
+hipError_t touch_code_object_spectral_gen();
+hipError_t touch_code_object_mnl();
+hipError_t touch_code_object_mnl_duo();
+hipError_t touch_code_object_fp64();
+}  // namespace tr

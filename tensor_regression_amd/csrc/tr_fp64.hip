@@ -391,3 +391,12 @@ hipError_t launch64_update(const FactorSet& fs, int n_bias, double* params, cons
 }
 
 }  // namespace tr
+
+namespace tr {
+// this translation unit's code object, loaded when the first plan is created (tr_api.hip:
+// preload_code_objects) instead of at the first launch of one of its kernels
+hipError_t touch_code_object_fp64() {
+  hipFuncAttributes a;
+  return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&k64_prep));
+}
+}  // namespace tr

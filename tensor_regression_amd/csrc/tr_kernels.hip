@@ -1412,3 +1412,12 @@ hipError_t launch_mttkrp(const FactorSet& fs, const float* phi, const float* dph
 }
 
 }  // namespace tr
+
+namespace tr {
+// this translation unit's code object, loaded when the first plan is created (tr_api.hip:
+// preload_code_objects) instead of at the first launch of one of its kernels
+hipError_t touch_code_object_kernels() {
+  hipFuncAttributes a;
+  return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&k_build_dense));
+}
+}  // namespace tr

@@ -756,3 +756,12 @@ extern "C" int tr_mnl_profile_read(unsigned long long* out) {
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mnl_prof), sizeof(g_mnl_prof));
 }
 #endif
+
+namespace tr {
+// this translation unit's code object, loaded when the first plan is created (tr_api.hip:
+// preload_code_objects) instead of at the first launch of one of its kernels
+hipError_t touch_code_object_mnl() {
+  hipFuncAttributes a;
+  return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&k_mnl_fused<true, 2>));
+}
+}  // namespace tr

@@ -966,3 +966,12 @@ hipError_t launch_spec_chain(int64_t n, const float* G, const float* dphi, float
 }
 
 }  // namespace tr
+
+namespace tr {
+// this translation unit's code object, loaded when the first plan is created (tr_api.hip:
+// preload_code_objects) instead of at the first launch of one of its kernels
+hipError_t touch_code_object_spectral() {
+  hipFuncAttributes a;
+  return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&k_spec_prep));
+}
+}  // namespace tr

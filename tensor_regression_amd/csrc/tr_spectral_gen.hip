@@ -404,3 +404,12 @@ hipError_t launch_specg(int mode, const SpecGeom& g, int nchunks, const float* X
 }
 
 }  // namespace tr
+
+namespace tr {
+// this translation unit's code object, loaded when the first plan is created (tr_api.hip:
+// preload_code_objects) instead of at the first launch of one of its kernels
+hipError_t touch_code_object_spectral_gen() {
+  hipFuncAttributes a;
+  return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&k_specg_epi<SPEC_TRAIN>));
+}
+}  // namespace tr

@@ -359,3 +359,12 @@ hipError_t launch_update(const FactorSet& fs, int n_bias, float* params, const f
 }
 
 }  // namespace tr
+
+namespace tr {
+// this translation unit's code object, loaded when the first plan is created (tr_api.hip:
+// preload_code_objects) instead of at the first launch of one of its kernels
+hipError_t touch_code_object_update() {
+  hipFuncAttributes a;
+  return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&k_update));
+}
+}  // namespace tr
