@@ -47,6 +47,11 @@ __device__ unsigned long long g_duo_prof[512][4][4];
   do {                  \
   } while (0)
 #endif
+#ifndef TR_DUO_P1REG
+#define TR_DUO_P1REG 1  // 1: the T unit's Phi1 operand quads held in 64 VGPRs for the launch (not read from
+                        // the LDS table every step: a third of the operand bytes), X addresses formed per
+                        // step, read-ahead 3 / 3 steps to fit 256 registers (the (128, 64) shape only)
+#endif
 #ifndef TR_DUO_R8
 #define TR_DUO_R8 0  // 1: every wave owns all 8 ranks of a 64 x 32 X sub-block (duo8_body)
 #endif
@@ -260,9 +265,13 @@ __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, cons
       (int)(uint32_t)(uintptr_t)((const __attribute__((address_space(3))) float*)lds));
   // LDS read offsets (floats): T quad c4 of this lane's row at aoff[c4]; V quad of step st at
   // boff[st & 3] + 4 J st; Phi1 quad of step st at pb + 4 st
-  int aoff[16], boff[4];
+  constexpr bool P1R = TR_DUO_P1REG != 0 && JT == 64;  // (the (64, 128) shape spills one register with it)
+  int aoff[P1R ? 1 : 16], boff[4];
+  const int abase = (64 * ib + lane) * J + 64 * jb, c4s = 4 * c;  // (P1R: aoff of step st = abase + (c4s ^ 4 st))
+  if constexpr (!P1R) {
 #pragma unroll
-  for (int c4 = 0; c4 < 16; ++c4) aoff[c4] = (64 * ib + lane) * J + 64 * jb + 4 * (c4 ^ c);
+    for (int c4 = 0; c4 < 16; ++c4) aoff[c4] = (64 * ib + lane) * J + 64 * jb + 4 * (c4 ^ c);
+  }
 #pragma unroll
   for (int m = 0; m < 4; ++m) boff[m] = (64 * ib + grow) * J + 64 * jb + 4 * (c ^ (4 * m + grow));
   const int pb = rq * P1S + 64 * jb;
@@ -279,6 +288,12 @@ __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, cons
 
   __syncthreads();
   __builtin_amdgcn_s_waitcnt(0);  // retire the prologue's loads (the loop waits are counted)
+  float4 p1r[P1R ? 16 : 1];  // (P1R) the T unit's B operand quads of every step, for the launch
+  if constexpr (P1R) {
+#pragma unroll
+    for (int st = 0; st < 16; ++st) p1r[st] = *reinterpret_cast<const float4*>(sP1 + pb + 4 * st);
+    __builtin_amdgcn_s_waitcnt(0);
+  }
 
   du_f32x4 gT = du_f32x4{0.f, 0.f, 0.f, 0.f};  // dPhi0 rows x ranks of the T unit
   du_f32x4 gV[4];                                // dPhi1 of the V unit, by row class
@@ -403,18 +418,24 @@ __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, cons
     // operand quads read ahead of their MFMAs (bounded live registers)
     float4 xt[16], bq[16], xv[16];
     auto ldT = [&](int st) {
-      xt[st] = *reinterpret_cast<const float4*>(sb + aoff[st]);
-      bq[st] = *reinterpret_cast<const float4*>(sP1 + pb + 4 * st);
+      if constexpr (P1R) {
+        xt[st] = *reinterpret_cast<const float4*>(sb + abase + (c4s ^ (4 * st)));
+        bq[st] = p1r[st];
+      } else {
+        xt[st] = *reinterpret_cast<const float4*>(sb + aoff[st]);
+        bq[st] = *reinterpret_cast<const float4*>(sP1 + pb + 4 * st);
+      }
     };
     auto ldV = [&](int st) { xv[st] = *reinterpret_cast<const float4*>(sb + boff[st & 3] + 4 * J * st); };
+    constexpr int XLT = P1R ? 3 : XLA, XLV = P1R ? 3 : XL;  // read-ahead depths of this form
 #pragma unroll
-    for (int st = 0; st < XLA; ++st) ldT(st);
+    for (int st = 0; st < XLT; ++st) ldT(st);
 #pragma unroll
-    for (int st = 0; st < XL; ++st) ldV(st);
+    for (int st = 0; st < XLV; ++st) ldV(st);
 #pragma unroll
     for (int st = 0; st < 16; ++st) {
-      if (st + XLA < 16) ldT(st + XLA);
-      if (st + XL < 16) ldV(st + XL);
+      if (st + XLT < 16) ldT(st + XLT);
+      if (st + XLV < 16) ldV(st + XLV);
       if (!EARLY && st % DMA_EVERY == 0 && st / DMA_EVERY < 8)
         du_dma_s(goff[st / DMA_EVERY], psrc, pm0 + (uint32_t)(st / DMA_EVERY) * 4096u);
       if (!EARLY && PF > 0 && st == 8)
