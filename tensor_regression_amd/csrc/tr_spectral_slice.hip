@@ -79,6 +79,18 @@
                              // 16 tile pieces (its 128-B lines are then already on their way into L2)
                              // instead of before them (0: every tail dword was its own HBM sector miss)
 #endif
+#ifndef TR_SLICE_TAILAT
+#define TR_SLICE_TAILAT 1  // with TAILLAST: wave p issues its tail dwords right after its pieces of gradient
+                           // tile TQ p + TQ - 1 (the tiles holding its tail rows, whose 128-B lines the
+                           // pair waves 0 / 3 fetch at the same stage) instead of after tile 7
+#endif
+#ifndef TR_SLICE_TAILQ
+#define TR_SLICE_TAILQ -1  // >= 0: every wave issues its tail after tile TR_SLICE_TAILQ (one code copy)
+#endif
+#ifndef TR_SLICE_TAILBUF
+#define TR_SLICE_TAILBUF 1  // split kernels: the tail dwords through the sample's buffer descriptor, all 64
+                            // lanes (no lane branch, no 64-bit per-lane address)
+#endif
 #ifndef TR_SLICE_NOSEL
 #define TR_SLICE_NOSEL 1  // epilogue table reads without per-element lane masks (see tab8)
 #endif
@@ -328,6 +340,15 @@ __device__ __forceinline__ void sl_dma16(const float* gsrc, const float* lds_dst
 // byte address m0 + 16 * lane; no per-lane 64-bit address arithmetic at the call
 // (lds_b: the destination's LDS byte address, wave-uniform: formed from a 32-bit base and a
 // compile-time offset, no generic-pointer cast with its null check at every piece)
+// one dword per lane from buffer byte offset voff into LDS (lane L -> lds_b + 4 L); an offset past
+// the descriptor's range reads 0
+__device__ __forceinline__ void sl_dma4b(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t lds_b) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen lds" SL_NT "\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(rs), "s"(lds_b)
+               : "memory");
+}
 __device__ __forceinline__ void sl_dma16b(__amdgpu_buffer_rsrc_t rs, uint32_t soff, uint32_t voff, uint32_t lds_b) {
   uint32_t keep;
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds" SL_NT "\n\ts_mov_b32 m0, %0"
@@ -394,6 +415,7 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
   float* slice = lds + wv * SL_SLICE;
   const uint32_t slice_b = (uint32_t)__builtin_amdgcn_readfirstlane(sl_lds_addr(slice));  // its LDS byte address
   float* sTail = lds + SL_O_TAIL + wv * SL_TAIL;  // [Dt][TR]
+  const uint32_t tail_b = (uint32_t)__builtin_amdgcn_readfirstlane(sl_lds_addr(sTail));
   float* sEx = lds + SL_O_EX;                      // [8 waves][64 lanes][8]
   float* sTP = lds + SL_O_TP;                      // [2 rows][32 columns][8 waves]
   float* sPart = lds + SL_O_PART;                  // [Z 16 | V 16][8 waves]
@@ -532,7 +554,12 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
   };
   auto dma_tail = [&](int64_t n) {
     const int ln = sl_lane_now();  // the per-lane source is formed at the call (no live address pair)
-    if (ln < Dt * TR) {  // lane -> (row 128 + lane / TR, w offset lane % TR)
+    if (SP && TR_SLICE_TAILBUF) {
+      // lane -> (row 128 + lane / TR, w offset lane % TR) as below; lanes with lane / TR >= Dt read
+      // the next row's first columns (or 0 past the half) into tail slots nothing reads
+      const int tr = ln / TR, wo = ln - tr * TR;
+      sl_dma4b(rsrc_of(n), (uint32_t)(((TR * p + wo) * D + 128 + tr) * 4), tail_b);
+    } else if (ln < Dt * TR) {  // lane -> (row 128 + lane / TR, w offset lane % TR)
       const int tr = ln / TR, wo = ln - tr * TR;
       const int64_t w = wbase + TR * p + wo;
       sl_dma4(X + n * xld + w * D + 128 + tr, sTail);
@@ -542,11 +569,18 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
   // otherwise first (waiting for tile 0 also retires it: the f32 form reads it inside the loop)
   constexpr bool TAIL_LAST = SP && TR_SLICE_TAILLAST;
   constexpr int NTL = (TAIL_LAST && Dt > 0) ? 1 : 0;  // tail pieces issued after the tiles
+  // TR_SLICE_TAILAT: after tile qt instead (the forward's wait for tile q + 1 then counts the tail
+  // only while q + 1 <= qt)
+  constexpr bool TAIL_AT = TAIL_LAST && TR_SLICE_TAILAT;
+  const int qt = !TAIL_AT ? SL_TILES - 1 : TR_SLICE_TAILQ >= 0 ? TR_SLICE_TAILQ : TQ * p + TQ - 1;
   auto dma_sample = [&](int64_t n) {
     if (Dt > 0 && !TAIL_LAST) dma_tail(n);
 #pragma unroll
-    for (int q = 0; q < SL_TILES; ++q) dma_tile(n, q);
-    if (Dt > 0 && TAIL_LAST) dma_tail(n);
+    for (int q = 0; q < SL_TILES; ++q) {
+      dma_tile(n, q);
+      if (Dt > 0 && TAIL_AT && q == qt) dma_tail(n);
+    }
+    if (Dt > 0 && TAIL_LAST && !TAIL_AT) dma_tail(n);
   };
 
   __builtin_amdgcn_s_waitcnt(0);  // retire the prologue's loads (the loop's waits are counted)
@@ -613,7 +647,7 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
         if (q + 1 < ntl) {
           {
             SL_SUB_BEGIN();
-            sl_wait_vm((ntl - 2 - q) * 2 + NTL + npf);
+            sl_wait_vm((ntl - 2 - q) * 2 + (q + 1 <= qt ? NTL : 0) + npf);
             SL_SUB_END(1);
           }
 #pragma unroll
@@ -972,6 +1006,7 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
             }
             if (!(TR_SLICE_SKIP & 4)) gacc[q][0] = sl_mfma6<SL_XP(SP)>(af, ds, gacc[q][0]);
             if (has_next) dma_piece(nn, q, 1);
+            if (TAIL_AT && has_next && Dt > 0 && q == qt) dma_tail(nn);
             if (!(TR_SLICE_SKIP & 4)) {
               if constexpr (SL_LP(SP))
                 gacc[q][1] = sl_mfma_lp<SL_XP(SP)>(af, dl, gacc[q][1]);
@@ -986,7 +1021,7 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
         }
       }
       // (this wave's tail operands were read at the top of the phase, and its tile reads waited)
-      if (TAIL_LAST && has_next && Dt > 0) dma_tail(nn);
+      if (TAIL_LAST && !TAIL_AT && has_next && Dt > 0) dma_tail(nn);
     }
     SL_MARK(7);
   }
