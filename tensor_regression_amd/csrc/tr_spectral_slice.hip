@@ -91,6 +91,10 @@
 #define TR_SLICE_TAILBUF 1  // split kernels: the tail dwords through the sample's buffer descriptor, all 64
                             // lanes (no lane branch, no 64-bit per-lane address)
 #endif
+#ifndef TR_SLICE_TAILMASK
+#define TR_SLICE_TAILMASK 1  // TAILBUF: lanes past the Dt tail rows take an out-of-range offset (no request;
+                             // each active lane's dword is a line of its own in the memory pipeline)
+#endif
 #ifndef TR_SLICE_NOSEL
 #define TR_SLICE_NOSEL 1  // epilogue table reads without per-element lane masks (see tab8)
 #endif
@@ -556,9 +560,10 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
     const int ln = sl_lane_now();  // the per-lane source is formed at the call (no live address pair)
     if (SP && TR_SLICE_TAILBUF) {
       // lane -> (row 128 + lane / TR, w offset lane % TR) as below; lanes with lane / TR >= Dt read
-      // the next row's first columns (or 0 past the half) into tail slots nothing reads
+      // 0 (TR_SLICE_TAILMASK) or the next row's first columns into tail slots nothing reads
       const int tr = ln / TR, wo = ln - tr * TR;
-      sl_dma4b(rsrc_of(n), (uint32_t)(((TR * p + wo) * D + 128 + tr) * 4), tail_b);
+      const uint32_t off = (uint32_t)(((TR * p + wo) * D + 128 + tr) * 4);
+      sl_dma4b(rsrc_of(n), (TR_SLICE_TAILMASK && tr >= Dt) ? 0xFFFFFF00u : off, tail_b);
     } else if (ln < Dt * TR) {  // lane -> (row 128 + lane / TR, w offset lane % TR)
       const int tr = ln / TR, wo = ln - tr * TR;
       const int64_t w = wbase + TR * p + wo;
