@@ -1,8 +1,16 @@
 #!/usr/bin/env python3
 """Benchmark: CP tensor-regression fit_Adam iterations on MI355X (gfx950 HIP path).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5] [--scaling weak|strong]
+                    [--no-cpu-baseline]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N ...   (N > 1)
+
+--scaling weak (default): every rank holds the config's per-GPU sample count (c4: 16384);
+--scaling strong: the config's total (c4: the 131072 samples of BASELINE configs[3], 68.7 GB of X
+on one GPU at N = 1) split over the ranks.  Samples come from one synthetic global dataset
+(seeded by 4096-row blocks), so a rank's shard is the same rows whichever mode or N made it.
+For N > 1 the line carries a "ranks" block: RCCL's own rank count (ncclCommCount), the sampled
+all-reduce time per step, every rank's dominant-kernel average, time and rate.
 
 `--gpus N` outside a launcher (no WORLD_SIZE in the environment) starts the N ranks itself: one
 child process per GPU with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT
@@ -41,16 +49,19 @@ METRIC = "training samples/sec + achieved HBM GB/s, 3-D CP regression rank=8, 1/
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 CONFIGS = {
-    "c2": dict(kind="linear", rows=65536, dims=(256, 128), rank=8, expect="fused-1pass",
+    "c2": dict(kind="linear", rows=65536, total_rows=65536, dims=(256, 128), rank=8, expect="fused-1pass",
                workload="configs[1]: 3-D standard CP regression, X (65536, 256, 128) fp32 per GPU, rank 8, "
                         "MSE + L2 (lambda 0.01), Adam lr 0.01"),
-    "c3": dict(kind="multinomial", rows=65536, dims=(128, 64), rank=8, classes=10, expect="mnl-fused-1pass",
+    "c3": dict(kind="multinomial", rows=65536, total_rows=65536, dims=(128, 64), rank=8, classes=10,
+               expect="mnl-fused-1pass",
                workload="configs[2]: multinomial CP regression, X (65536, 128, 64) fp32 per GPU, 10 classes, "
                         "rank 8, softmax + weighted CE + L2, Adam lr 0.01"),
-    "c4": dict(kind="linear", rows=16384, dims=(64, 64, 32), rank=16, expect="cluster-1pass",
-               workload="configs[3]: 4-D CP regression, X (131072, 64, 64, 32) sharded 16384 samples per GPU, "
-                        "rank 16, Adam lr 0.01"),
-    "c5": dict(kind="spectral", rows=32768, dims=(256, 129), rank=8, rank_spectral=8, n_complex_dim=1, n_out=2,
+    "c4": dict(kind="linear", rows=16384, total_rows=131072, cpu_rows=16384, dims=(64, 64, 32), rank=16,
+               expect="cluster-1pass",
+               workload="configs[3]: 4-D CP regression, X (131072, 64, 64, 32) sharded 16384 samples per GPU "
+                        "(--scaling strong: the 131072 samples split over the ranks), rank 16, Adam lr 0.01"),
+    "c5": dict(kind="spectral", rows=32768, total_rows=32768, dims=(256, 129), rank=8, rank_spectral=8,
+               n_complex_dim=1, n_out=2,
                expect="slice-1pass-mfma",
                workload="configs[4]: spectral_tensor_regression.py fit_Adam, X (32768, 256, 129) fp32 (real: the "
                         "reference rejects complex X; |rfft|-like non-negative synthetic data), rank_normal = "
@@ -86,17 +97,41 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def make_data(cfg, rank_id, dev):
-    """Seeded synthetic shard for this rank: X ~ N(0,1), planted CP model, y / labels."""
-    g = torch.Generator(device=dev).manual_seed(1234 + rank_id)
-    N, dims, R = cfg["rows"], cfg["dims"], cfg["rank"]
+DATA_BLOCK = 4096  # rows per seeded generator block of the synthetic global dataset
+
+
+def shard_rows(total, world, rank_id):
+    """(row0, rows) of this rank's contiguous shard of `total` samples (the first total % world
+    ranks take one more)."""
+    base, extra = divmod(int(total), int(world))
+    rows = base + (1 if rank_id < extra else 0)
+    return rank_id * base + min(rank_id, extra), rows
+
+
+def _block_gen(dev, b):
+    return torch.Generator(device=dev).manual_seed(1234 + b)
+
+
+def make_data(cfg, rows, row0, dev):
+    """Seeded synthetic shard: global rows [row0, row0 + rows) of one synthetic dataset (X ~ N(0,1)
+    by DATA_BLOCK-row blocks, each from its own seed, so a sample is the same whatever the rank
+    count or the scaling mode), a planted CP model (identical on every rank) and y / labels."""
+    N, dims, R = rows, cfg["dims"], cfg["rank"]
     if cfg.get("windowed"):
         from tensor_regression_amd.util import windowed_view
         L = dims[0]
+        g = _block_gen(dev, 0)
         Xu = torch.randn((N + L - 1,) + tuple(dims[1:]), device=dev, generator=g, dtype=torch.float32)
         X, _ = windowed_view(Xu, torch.zeros(N + L - 1, device=dev), (0, L))
     else:
-        X = torch.randn((N,) + tuple(dims), device=dev, generator=g, dtype=torch.float32)
+        X = torch.empty((N,) + tuple(dims), device=dev, dtype=torch.float32)
+        for b in range(row0 // DATA_BLOCK, -(-(row0 + N) // DATA_BLOCK)):
+            blk = torch.randn((DATA_BLOCK,) + tuple(dims), device=dev, generator=_block_gen(dev, b),
+                              dtype=torch.float32)
+            lo, hi = max(row0, b * DATA_BLOCK), min(row0 + N, (b + 1) * DATA_BLOCK)
+            X[lo - row0:hi - row0] = blk[lo - b * DATA_BLOCK:hi - b * DATA_BLOCK]
+            del blk
+    gn = torch.Generator(device=dev).manual_seed(4321 + row0)  # noise / label draws of this shard
     gc = torch.Generator().manual_seed(99)  # planted factors identical on every rank
     if cfg["kind"] == "spectral":
         from tensor_regression_amd.spectral_tensor_regression import lin_model as spec_lin
@@ -104,20 +139,21 @@ def make_data(cfg, rank_id, dev):
         O = cfg["n_out"]
         A = [(torch.randn(d, R, 1, generator=gc) / 8).to(dev) for d in dims] + [torch.randn(O, R, 1, generator=gc).to(dev)]
         y = spec_lin(X, A, torch.ones(R, device=dev), [False] * 3, torch.zeros(O, device=dev))
-        y = y + 0.1 * torch.randn(N, O, device=dev, generator=g)
+        y = y + 0.1 * torch.randn(N, O, device=dev, generator=gn)
         return X, y
     if cfg["kind"] == "linear":
         from tensor_regression_amd.standard_tensor_regression import lin_model
         A = [(torch.randn(d, R, generator=gc) / 4).to(dev) for d in dims]
         y = lin_model(X, A, torch.ones(R, device=dev), [False] * len(A), torch.zeros(1, device=dev))
-        y = y + 0.1 * torch.randn(N, device=dev, generator=g)
+        y = y + 0.1 * torch.randn(N, device=dev, generator=gn)
         return X, y
     from tensor_regression_amd.multinomial_tensor_regression import model as mnl_model
     C = cfg["classes"]
     A = [(torch.randn(d, R, generator=gc) / 3).to(dev) for d in dims] + [torch.randn(C, R, generator=gc).to(dev)]
     S = mnl_model(X, A, torch.ones(R, device=dev), [False] * len(A))
-    y = torch.multinomial(S, 1, generator=g).reshape(-1)
-    y[:C] = torch.arange(C, device=dev)
+    y = torch.multinomial(S, 1, generator=gn).reshape(-1)
+    if N >= C:
+        y[:C] = torch.arange(C, device=dev)  # every class present in every shard
     return X, y
 
 
@@ -157,6 +193,9 @@ def cpu_baseline(cfg, X, y, model_init, budget_s=15.0, threads=None):
     quota = os.environ.get("OMP_NUM_THREADS")
     nthreads = threads or (int(quota) if quota and quota.isdigit() else info["affinity_cpus"])
     torch.set_num_threads(nthreads)
+    cap = cfg.get("cpu_rows")
+    if cap and X.shape[0] > cap:  # bounded sample of the workload: the first cap samples
+        X, y = X[:cap], y[:cap]
     Xc = X.cpu()
     yc = y.cpu()
     R = cfg["rank"]
@@ -198,7 +237,9 @@ def cpu_baseline(cfg, X, y, model_init, budget_s=15.0, threads=None):
             if spread > 2.0 else "")
     return {"value": N / med, "unit": "samples/s", "cores": torch.get_num_threads(), "kind": "port",
             "sample": f"oracle/cp_oracle.py fit_Adam (torch {torch.__version__} CPU, the reference's op order) on "
-                      f"the same {N} x {list(cfg['dims'])} X (full per-GPU size): {iters} iterations each timed "
+                      f"the same {N} x {list(cfg['dims'])} X ("
+                      f"{'full per-GPU size' if not cap or N < cap else f'the first {N} samples of the GPU shard'}"
+                      f"): {iters} iterations each timed "
                       f"alone after 2 warm-up ({t.sum():.1f} s), value = N / median iteration time, "
                       f"torch.set_num_threads({nthreads}) "
                       f"({'OMP_NUM_THREADS quota of this job' if threads is None and quota else 'threads'})" + note,
@@ -260,10 +301,14 @@ def host_stream_report(model, hs, Xres, y, fit, ms_step, dev):
             "overlap_hidden_frac": overlap, "chunk_rows": hs.chunk_rows, "bytes_per_step": nbytes}
 
 
-def launch_ranks(n, argv, json_out):
+def launch_ranks(n, argv, json_out, timeout=None, cmd=None, grace=10.0):
     """Start the N ranks of `bench.py --gpus N` as child processes (torchrun's environment; the
     parent makes no HIP call: torch.cuda.device_count() does not initialise HIP on this image).
-    Returns the exit code; rank 0's stdout (the JSON line) is written only if every rank succeeded."""
+    Returns the exit code; rank 0's stdout (the JSON line) is written only if every rank succeeded.
+    `timeout` (seconds, --launch-timeout) bounds the whole run: past it the ranks still running
+    are terminated, killed after `grace` seconds, and the run fails (a rank stuck in rendezvous
+    or communicator set-up, before the fit's RCCL watchdog applies, cannot hang the parent).
+    `cmd` replaces the child command (tests)."""
     import socket
     import subprocess
     visible = torch.cuda.device_count()
@@ -278,10 +323,12 @@ def launch_ranks(n, argv, json_out):
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
+        procs.append(subprocess.Popen((cmd or [sys.executable, os.path.abspath(__file__)]) + argv, env=env,
                                       stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
     rc = 0
     pending = set(range(n))
+    t_end = None if timeout is None else time.monotonic() + timeout
+    killed_at = None
     while pending:
         for r in sorted(pending):
             code = procs[r].poll()
@@ -293,12 +340,47 @@ def launch_ranks(n, argv, json_out):
                 log(f"bench: rank {r} exited with {code}; stopping the other ranks")
                 for q in pending:
                     procs[q].terminate()
+                killed_at = time.monotonic()
+        now = time.monotonic()
+        if pending and t_end is not None and now > t_end and killed_at is None:
+            log(f"bench: the {n}-rank run exceeded --launch-timeout {timeout:.0f} s; terminating ranks "
+                f"{sorted(pending)}")
+            rc = rc or 124
+            for q in pending:
+                procs[q].terminate()
+            killed_at = now
+        if pending and killed_at is not None and now > killed_at + grace:
+            for q in pending:
+                procs[q].kill()
         time.sleep(0.05)
     out = procs[0].stdout.read().decode()
     if rc == 0:
         json_out.write(out)
         json_out.flush()
     return rc
+
+
+def rank_summary(world, rows, el_s, dom_ms, steps, comm_ranks, allreduce_samples, arena_bytes, scaling):
+    """The N > 1 block of the JSON line from every rank's numbers (index = rank): what the driver's
+    scaling run must show, from the run itself — the communicator's own rank count (ncclCommCount),
+    the sampled all-reduce time per step, the spread of the dominant kernel over the ranks, and
+    each rank's own rate.  allreduce_samples: [(ms, bytes)] sampled on rank 0."""
+    ar_us = [1e3 * ms for ms, _ in allreduce_samples]
+    return {
+        "world_size": world,
+        "scaling": scaling,
+        "rccl_ranks": comm_ranks,
+        "rows_per_rank": [int(r) for r in rows],
+        "allreduce_us_per_step": float(np.median(ar_us)) if ar_us else None,
+        "allreduce_us_range": [float(min(ar_us)), float(max(ar_us))] if ar_us else None,
+        "allreduce_samples": len(ar_us),
+        "allreduce_bytes": int(allreduce_samples[0][1]) if allreduce_samples else arena_bytes,
+        "dominant_kernel_ms_min": float(min(dom_ms)),
+        "dominant_kernel_ms_max": float(max(dom_ms)),
+        "dominant_kernel_ms_per_rank": [float(v) for v in dom_ms],
+        "per_rank_ms_per_step": [1e3 * float(e) / steps for e in el_s],
+        "per_rank_samples_per_s": [float(r) * steps / float(e) for r, e in zip(rows, el_s)],
+    }
 
 
 def main():
@@ -326,6 +408,13 @@ def main():
                     help="bracket only every n-th launch of the timed kernels with HIP events (default: every launch)")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="no hipEvents in the timed region (ms_per_step without event packets; no roofline)")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="weak (default): every rank holds the config's per-GPU sample count; strong: the config's "
+                         "total sample count (c4: 131072) split over the ranks")
+    ap.add_argument("--launch-timeout", type=float, default=1800.0,
+                    help="self-launched N > 1 runs: seconds before the remaining ranks are terminated (exit non-zero)")
+    ap.add_argument("--allreduce-sample-every", type=int, default=5,
+                    help="N > 1: time every n-th gradient all-reduce of the timed fit with HIP events")
     ap.add_argument("--traffic", default=os.path.join(HERE, "profiles", "traffic.json"),
                     help="PMC traffic summary (tools/pmc_traffic.py output) for the roofline 'traffic' field")
     args = ap.parse_args()
@@ -335,7 +424,7 @@ def main():
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
     if env_world is None and args.gpus > 1:
-        sys.exit(launch_ranks(args.gpus, sys.argv[1:], json_out))
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:], json_out, timeout=args.launch_timeout))
     if env_world is not None and int(env_world) != args.gpus:
         log(f"bench: --gpus {args.gpus} but the launcher started WORLD_SIZE={env_world} ranks; no measurement")
         sys.exit(2)
@@ -357,7 +446,14 @@ def main():
 
     from tensor_regression_amd import CP_linear_regression, CP_logistic_regression
 
-    X, y = make_data(cfg, rank_id, dev)
+    if args.scaling == "strong":
+        if cfg.get("windowed") or cfg.get("hoststream"):
+            ap.error(f"--scaling strong is not defined for {args.config}")
+        row0, rows = shard_rows(cfg["total_rows"], world, rank_id)
+    else:
+        rows = cfg["rows"]
+        row0 = rank_id * rows
+    X, y = make_data(cfg, rows, row0, dev)
     torch.cuda.synchronize()
     Xres = X  # the device-resident X (hoststream: for the copy / compute-only reference timings)
     if cfg.get("hoststream"):
@@ -425,6 +521,15 @@ def main():
         if pg is not None:
             torch.distributed.barrier()
 
+    comm = None
+    if pg is not None and world > 1:
+        from tensor_regression_amd import _engine
+        comm = _engine.gradient_allreduce(pg, local)
+        if isinstance(comm, _engine.RcclAllReduce):
+            comm.set_timing(args.allreduce_sample_every)
+        else:
+            comm = None
+
     _ph("set_timing")
     barrier()
     torch.cuda.synchronize()
@@ -436,20 +541,25 @@ def main():
     el = time.perf_counter() - t0
     plan.set_timing(False)
     kt = plan.read_timing()
-    if pg is not None:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        el = float(t.item())
+    ar_samples = []
+    if comm is not None:
+        ar_samples = comm.read_timing()
+        comm.set_timing(0)
+    el_local = el
     N = X.shape[0]
     P = int(np.prod(cfg["dims"]))
-    ms_step = 1e3 * el / args.steps
-    value = world * N * args.steps / el
-    hoststream = host_stream_report(model, X, Xres, y, fit, ms_step, dev) if cfg.get("hoststream") else None
 
     if args.no_kernel_timing:
+        tot = float(N)
+        if pg is not None:
+            t = torch.tensor([el, float(N)], dtype=torch.float64, device=dev)
+            torch.distributed.all_reduce(t[:1], op=torch.distributed.ReduceOp.MAX)
+            torch.distributed.all_reduce(t[1:], op=torch.distributed.ReduceOp.SUM)
+            el, tot = float(t[0]), float(t[1])
         if rank_id == 0:
-            json_out.write(json.dumps({"metric": METRIC, "value": value, "unit": "samples/s", "n_gpus": world,
-                                       "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step,
+            json_out.write(json.dumps({"metric": METRIC, "value": tot * args.steps / el, "unit": "samples/s",
+                                       "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                                       "ms_per_step": 1e3 * el / args.steps, "scaling": args.scaling,
                                        "config": {"workload": cfg["workload"], "plan": plan.describe},
                                        "roofline": None, "note": "--no-kernel-timing"}) + "\n")
             json_out.flush()
@@ -489,6 +599,26 @@ def main():
         if dom == "stream_rows" and "+mfma-fwd" in plan.describe:
             dom_name = "k_rows_mfma"
     dom_ms = kernel_avg[dom]
+    ranks_block = None
+    rows_all = [N]
+    if pg is not None:
+        # every rank's wall time, dominant-kernel average and rows (value uses the max wall time)
+        t = torch.tensor([el_local, dom_ms, float(N)], dtype=torch.float64, device=dev)
+        parts = [torch.zeros_like(t) for _ in range(world)]
+        torch.distributed.all_gather(parts, t)
+        el_all = [float(p[0]) for p in parts]
+        dom_all = [float(p[1]) for p in parts]
+        rows_all = [int(p[2]) for p in parts]
+        el = max(el_all)
+        if world > 1:
+            ranks_block = rank_summary(world, rows_all, el_all, dom_all, args.steps,
+                                       comm.count() if comm is not None else None, ar_samples,
+                                       plan.num_grads * 4, args.scaling)
+            if comm is None:
+                ranks_block["note"] = "torch.distributed all_reduce path (TR_RCCL_DIRECT=0): no RCCL count / timing"
+    ms_step = 1e3 * el / args.steps
+    value = sum(rows_all) * args.steps / el
+    hoststream = host_stream_report(model, X, Xres, y, fit, ms_step, dev) if cfg.get("hoststream") else None
     achieved = bytes_launch / (dom_ms * 1e-3) / 1e9
     traffic = None
     traffic_src = None
@@ -513,12 +643,12 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "fp32",
         "data": "synthetic (seeded torch.randn X on device, planted CP model + noise)",
         "config": {"workload": cfg["workload"], "samples_per_gpu": N, "feature_dims": list(cfg["dims"]),
-                   "rank": R, "global_batch": world * N,
+                   "rank": R, "global_batch": sum(rows_all),
                    "parallelism": f"dp{world} sample-sharded, one RCCL all-reduce of the gradient arena per step",
                    "plan": plan.describe},
         "achieved_hbm_GBps_per_gpu": iter_bytes / (ms_step * 1e-3) / 1e9,
@@ -559,6 +689,10 @@ def main():
             xp = "three" if "xpieces=3" in plan.describe else "two"
             out["roofline"]["gemm_form"] = (f"bf16 split GEMMs: factor-side operands in three RNE bf16 pieces, X in "
                                             f"{xp}, fp32 accumulate")
+            # the arithmetic is not plain fp32 GEMMs: say so in the field consumers read
+            out["dtype"] = f"fp32 (GEMMs on bf16 pieces: X in {xp}, factors in three; fp32 accumulate)"
+    if ranks_block is not None:
+        out["ranks"] = ranks_block
     if rank_id == 0 and world == 1 and not args.no_cpu_baseline:
         log("cpu baseline ...")
         out["cpu_baseline"] = cpu_baseline(cfg, Xres, y, init, args.cpu_budget, args.cpu_threads)

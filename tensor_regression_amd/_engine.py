@@ -613,10 +613,45 @@ def _rccl_lib():
     lib.ncclGetErrorString.argtypes = [ctypes.c_int]
     lib.ncclCommGetAsyncError.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
     lib.ncclCommAbort.argtypes = [ctypes.c_void_p]
+    lib.ncclCommCount.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
     for fn in ("ncclGetUniqueId", "ncclCommInitRank", "ncclAllReduce", "ncclCommDestroy", "ncclCommGetAsyncError",
-               "ncclCommAbort"):
+               "ncclCommAbort", "ncclCommCount"):
         getattr(lib, fn).restype = ctypes.c_int
     return lib
+
+
+class _CollectiveTimeout(Exception):
+    pass
+
+
+class _CollectiveError(Exception):
+    pass
+
+
+def wait_progress(events, async_error, timeout, clock=None, sleep=None):
+    """Poll `events` (objects with .query(), completing in order: one per all-reduce, the last one
+    behind all queued work) until every one has completed.  Raise _CollectiveError as soon as
+    `async_error()` reports an error, and _CollectiveTimeout when `timeout` seconds pass in which
+    no further event completed: the clock restarts at every completed event, so the bound is on
+    time WITHOUT progress, whatever the number of iterations between host syncs."""
+    import time
+    clock = time.monotonic if clock is None else clock
+    sleep = time.sleep if sleep is None else sleep
+    i, n = 0, len(events)
+    t0 = clock()
+    spins = 0
+    while i < n:
+        if events[i].query():
+            i += 1
+            t0 = clock()
+            continue
+        msg = async_error()
+        if msg is not None:
+            raise _CollectiveError(msg)
+        if clock() - t0 > timeout:
+            raise _CollectiveTimeout(f"{i} of the {n} queued steps had completed")
+        spins += 1
+        sleep(0 if spins < 2000 else 1e-4)
 
 
 class RcclAllReduce:
@@ -642,6 +677,8 @@ class RcclAllReduce:
         buf = torch.frombuffer(bytearray(uid_to_bytes(uid)), dtype=torch.uint8).to(f"cuda:{self.dev}")
         dist.broadcast(buf, src=ranks[0], group=process_group)
         uid = uid_from_bytes(buf.cpu().numpy().tobytes())
+        self._pending, self._free = [], []  # watchdog events: recorded / completed and reusable
+        self._t_every, self._t_calls, self._t_pairs = 0, 0, []  # sampled all-reduce timing (bench.py)
         self.comm = ctypes.c_void_p()
         with torch.cuda.device(self.dev):
             self._check(self.lib.ncclCommInitRank(ctypes.byref(self.comm), len(ranks), uid, me), "ncclCommInitRank")
@@ -653,34 +690,70 @@ class RcclAllReduce:
     def __call__(self, t):
         dt = {torch.float32: 7, torch.float64: 8}[t.dtype]  # ncclFloat32 / ncclFloat64
         p = ctypes.c_void_p(t.data_ptr())
+        timed = self._t_every > 0 and self._t_calls % self._t_every == 0
+        self._t_calls += 1
+        if timed:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(torch.cuda.current_stream(self.dev))
         self._check(self.lib.ncclAllReduce(p, p, t.numel(), dt, 0, self.comm, stream_handle(self.dev)),
                     "ncclAllReduce")
+        if timed:
+            e1.record(torch.cuda.current_stream(self.dev))
+            self._t_pairs.append((e0, e1, t.numel() * t.element_size()))
+        if self.size > 1:  # progress marker for the watchdog: one event behind every all-reduce
+            ev = self._free.pop() if self._free else torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.dev))
+            self._pending.append(ev)
 
     def wait(self, timeout=None):
         """Block until the work queued on the current stream (this rank's all-reduces included) has
-        finished, polling the communicator: an asynchronous RCCL error or `timeout` seconds
-        (TR_RCCL_TIMEOUT, default 600) without progress aborts the communicator and raises, so a
-        rank whose peer died does not hang in the next host sync.  ProcessGroupNCCL's watchdog does
-        this for torch's own collectives; this communicator is outside it."""
-        import time
+        finished, polling the communicator: an asynchronous RCCL error, or `timeout` seconds
+        (TR_RCCL_TIMEOUT, default 600) in which no further all-reduce of this rank completed,
+        aborts the communicator and raises, so a rank whose peer died does not hang in the next
+        host sync.  Progress is counted per all-reduce (one event behind each), not per host sync:
+        a slow but healthy chunk of sync_every iterations never trips it.  ProcessGroupNCCL's
+        watchdog does this for torch's own collectives; this communicator is outside it."""
         timeout = _RCCL_TIMEOUT if timeout is None else timeout
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(self.dev))
-        t0 = time.monotonic()
-        spins = 0
-        while not ev.query():
-            err = ctypes.c_int(0)
-            rc = self.lib.ncclCommGetAsyncError(self.comm, ctypes.byref(err))
-            if rc != 0 or err.value not in (0, 7):  # 7 = ncclInProgress
-                self.abort()
-                raise RuntimeError(f"RCCL all-reduce of the sharded fit failed asynchronously: "
-                                   f"{self.lib.ncclGetErrorString(err.value or rc).decode()}")
-            if time.monotonic() - t0 > timeout:
-                self.abort()
-                raise RuntimeError(f"RCCL all-reduce of the sharded fit made no progress for {timeout:.0f} s "
-                                   "(a peer rank died or left the fit); the communicator was aborted")
-            spins += 1
-            time.sleep(0 if spins < 2000 else 1e-4)
+        tail = self._free.pop() if self._free else torch.cuda.Event()
+        tail.record(torch.cuda.current_stream(self.dev))
+        pending, self._pending = self._pending + [tail], []
+        try:
+            wait_progress(pending, self._async_error, timeout)
+        except _CollectiveTimeout as e:
+            self.abort()
+            raise RuntimeError(f"RCCL all-reduce of the sharded fit made no progress for {timeout:.0f} s "
+                               f"({e}; a peer rank died or left the fit); the communicator was aborted") from None
+        except _CollectiveError as e:
+            self.abort()
+            raise RuntimeError(f"RCCL all-reduce of the sharded fit failed asynchronously: {e}") from None
+        self._free.extend(pending)
+
+    def count(self):
+        """Ranks of the communicator (ncclCommCount): what RCCL itself sees, not the torch group."""
+        n = ctypes.c_int(0)
+        self._check(self.lib.ncclCommCount(self.comm, ctypes.byref(n)), "ncclCommCount")
+        return int(n.value)
+
+    def set_timing(self, every):
+        """Bracket every `every`-th all-reduce with timing events (0: off; bench.py's N > 1 line)."""
+        self._t_every, self._t_calls, self._t_pairs = max(0, int(every)), 0, []
+
+    def read_timing(self):
+        """[(ms, bytes)] of the sampled all-reduces since set_timing (synchronises their events)."""
+        out = []
+        for e0, e1, nb in self._t_pairs:
+            e1.synchronize()
+            out.append((e0.elapsed_time(e1), nb))
+        self._t_pairs = []
+        return out
+
+    def _async_error(self):
+        """None while the communicator is healthy, else RCCL's error string."""
+        err = ctypes.c_int(0)
+        rc = self.lib.ncclCommGetAsyncError(self.comm, ctypes.byref(err))
+        if rc != 0 or err.value not in (0, 7):  # 7 = ncclInProgress
+            return self.lib.ncclGetErrorString(err.value or rc).decode()
+        return None
 
     def abort(self):
         if self.comm is not None and self.comm.value:

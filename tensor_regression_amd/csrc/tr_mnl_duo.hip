@@ -52,9 +52,6 @@ __device__ unsigned long long g_duo_prof[512][4][4];
                         // the LDS table every step: a third of the operand bytes), X addresses formed per
                         // step, read-ahead 3 / 3 steps to fit 256 registers (the (128, 64) shape only)
 #endif
-#ifndef TR_DUO_R8
-#define TR_DUO_R8 0  // 1: every wave owns all 8 ranks of a 64 x 32 X sub-block (duo8_body)
-#endif
 #ifndef TR_DUO_SKIP
 #define TR_DUO_SKIP 0  // profiling ablation only (results invalid): 1 loop LDS-DMA, 2 MFMAs, 4 epilogue
 #endif
@@ -83,10 +80,6 @@ constexpr bool EARLY = TR_DUO_EARLY != 0;
 #define TR_DUO_XLA 4
 #endif
 constexpr int XLA = TR_DUO_XLA;  // the same for the A-waves (X and Phi1 quads)
-#ifndef TR_DUO_XL8
-#define TR_DUO_XL8 4
-#endif
-constexpr int XL8 = TR_DUO_XL8;  // TR_DUO_R8: iterations the operand reads run ahead of their MFMAs
 #ifndef TR_DUO_SB
 #define TR_DUO_SB 1
 #endif
@@ -546,373 +539,6 @@ __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, cons
   for (int64_t e = t; e < g.slab; e += DU_T) slab[e] = sG[e];
 }
 
-// ------------------------------------------------------------------------------------------
-// TR_DUO_R8: every wave owns ALL 8 ranks of a 64 x 32 X sub-block (rows 64 ib .. +63, columns
-// 32 jq .. +31; J = 64: ib = wv & 1, jq = wv >> 1; J = 128: ib = 0, jq = wv), so each X element is
-// read from LDS by one wave for its T unit and once for its V unit (the rank-block form above
-// reads it four times: both units of both rank-block waves of its 64 x 64 block):
-//  - T unit (lane = row): 8 steps of one column quad, 8 MFMAs each (4 columns x 2 rank blocks),
-//    Phi1 from the transposed table (one quad per rank block and step);
-//  - V unit (row class grow, lane c: column quad c & 7 of the wave's 8, rank block hv = c >> 3):
-//    16 steps of 4 rows, each lane reads HALF its quad (elements 2 hv, 2 hv + 1: ds_read_b64) and
-//    takes the other half from lane c ^ 8 (DPP row_ror:8); accumulator k then holds element
-//    k ^ (2 hv) of the quad, so the two halves need no select.
-// T and V are partials over the wave's columns / rows: U, the Z partials (one slot per wave) and
-// the dPhi0 / dPhi1 / dPhiC accumulators are linear in them and are summed in wave order at the
-// end, like the rank-block form's.  LDS operand bytes per wave and sample: 8 KiB T rows + 8 KiB V
-// halves + 16 KiB Phi1 quads (48 KiB in the rank-block form).
-// ------------------------------------------------------------------------------------------
-template <int JT>
-__device__ __forceinline__ void duo8_body(const MnlGeom& g, const DuArgs& a, const int64_t* __restrict__ lab,
-                                          const float* __restrict__ class_w, float* lds, const int wv, const int lane) {
-  const int t = threadIdx.x;
-  constexpr int J = JT, I = 8192 / JT, SPF = 8192, JQ = J / 4;
-  constexpr int NIB = I / 64;
-  const int R = g.R, C = g.C;
-  float* sZ = lds + g.du_oZ;    // [2 parity][16 classes][4 wave slots]
-  float* sP1 = lds + g.du_oP1;  // Phi1^T [8][J + 4]
-  constexpr int P1S = J + 4;
-  const float* P0 = a.phi;
-  const float* P1 = a.phi + g.offP1;
-  const float* PC = a.phi + g.offPC;
-  const int c = lane & 15, grow = lane >> 4, l3 = lane & 3;
-  const bool cok = c < C;
-  const float cwl = cok ? class_w[c] : 0.f;
-  const float NEG = -__builtin_huge_valf();
-  float sel[4], gsel[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    sel[q] = l3 == q ? 1.f : 0.f;
-    gsel[q] = grow == q ? 1.f : 0.f;
-  }
-  const int ib = NIB == 2 ? (wv & 1) : 0;
-  const int jq = NIB == 2 ? (wv >> 1) : wv;
-  const int hv = c >> 3;
-  // T unit: U weights phiU[rb][v] = Phi0[64 ib + 4 (l >> 2) + v][4 rb + l3]
-  float phiU[2][4];
-#pragma unroll
-  for (int rb = 0; rb < 2; ++rb)
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const int r = 4 * rb + l3;
-      phiU[rb][v] = r < R ? P0[(int64_t)(64 * ib + 4 * (lane >> 2) + v) * R + r] : 0.f;
-    }
-  float wpc[8];  // w_r PhiC[c][r]
-#pragma unroll
-  for (int r = 0; r < 8; ++r) wpc[r] = (cok && r < R) ? a.w[r] * PC[c * R + r] : 0.f;
-  float pcg[2], wg[2];  // epilogue weights of rank 4 rb + grow
-#pragma unroll
-  for (int rb = 0; rb < 2; ++rb) {
-    const int rg = 4 * rb + grow;
-    pcg[rb] = (cok && rg < R) ? a.w[rg] * PC[c * R + rg] : 0.f;
-    wg[rb] = rg < R ? a.w[rg] : 0.f;
-  }
-  // V unit: B operand Phi0[64 ib + 4 st + grow][4 hv + l3]
-  const int rv = 4 * hv + l3;
-  float bopB[16];
-#pragma unroll
-  for (int st = 0; st < 16; ++st) bopB[st] = rv < R ? P0[(int64_t)(64 * ib + 4 * st + grow) * R + rv] : 0.f;
-  for (int e = t; e < 8 * J; e += DU_T) {
-    const int r = e / J, j = e - r * J;
-    sP1[r * P1S + j] = r < R ? P1[(int64_t)j * R + r] : 0.f;
-  }
-  for (int e = t; e < 2 * 16 * 4; e += DU_T) sZ[e] = 0.f;
-
-  uint32_t goff[8];  // LDS-DMA map: as the rank-block form
-#pragma unroll
-  for (int gi = 0; gi < 8; ++gi) {
-    const int slot = (wv + DU_NW * gi) * TR_WAVE + lane;
-    const int i = slot / JQ;
-    const int q = slot - i * JQ;
-    goff[gi] = 4u * (uint32_t)(i * J + 4 * (q ^ (i & 15)));
-  }
-  const uint32_t lbase = (uint32_t)__builtin_amdgcn_readfirstlane(
-      (int)(uint32_t)(uintptr_t)((const __attribute__((address_space(3))) float*)lds));
-  // LDS read offsets (floats): T row 64 ib + lane, global quad 8 jq + s at swizzled position
-  // (8 jq + s) ^ c; V row 64 ib + 4 st + grow (i & 15 = 4 (st & 3) + grow), global quad 8 jq +
-  // (c & 7), half hv; Phi1 quad of rank block rb at pb[rb] + 4 s
-  int aoff[8], boff[4];
-#pragma unroll
-  for (int s = 0; s < 8; ++s) aoff[s] = (64 * ib + lane) * J + 4 * ((8 * jq + s) ^ c);
-#pragma unroll
-  for (int m = 0; m < 4; ++m) boff[m] = (64 * ib + grow) * J + 4 * ((8 * jq + (c & 7)) ^ (4 * m + grow)) + 2 * hv;
-  const int pb0 = l3 * P1S + 32 * jq, pb1 = (4 + l3) * P1S + 32 * jq;
-  const uint32_t pfoff = 128u * (uint32_t)(wv * TR_WAVE + lane);
-  const uint32_t pfm0 = lbase + 4u * (uint32_t)g.du_oPF;
-
-  const int64_t n0 = IL ? (int64_t)blockIdx.x : (int64_t)blockIdx.x * a.rows_per_wg;
-  const int64_t G = IL ? (int64_t)gridDim.x : 1;
-  const int64_t n1 = IL ? a.N : (n0 + a.rows_per_wg < a.N ? n0 + a.rows_per_wg : a.N);
-  const int nr = (int)(n1 > n0 ? (n1 - n0 + G - 1) / G : 0);
-  auto sample_of = [&](int k) -> int64_t { return n0 + G * (a.reverse ? (nr - 1 - k) : k); };
-  auto src_of = [&](int k) -> const float* { return a.X + sample_of(k) * a.xld; };
-
-  __syncthreads();
-  __builtin_amdgcn_s_waitcnt(0);
-
-  du_f32x4 gT[2], gV[4];
-#pragma unroll
-  for (int q = 0; q < 2; ++q) gT[q] = du_f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int q = 0; q < 4; ++q) gV[q] = du_f32x4{0.f, 0.f, 0.f, 0.f};
-  float dpc[2] = {0.f, 0.f};
-  double lsum = 0.0;
-
-  du_f32x4 TP[2], VP[4];
-#pragma unroll
-  for (int q = 0; q < 2; ++q) TP[q] = du_f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int q = 0; q < 4; ++q) VP[q] = du_f32x4{0.f, 0.f, 0.f, 0.f};
-  float uP[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-  int64_t yP = 0;
-  float cwP = 0.f;
-
-  // epilogue (the rank-block form's 8 stages; the rank-dependent class sums and Wv for both
-  // rank blocks)
-  float4 e_zp = make_float4(0.f, 0.f, 0.f, 0.f);
-  float e_x = 0.f, e_ez = 0.f, e_sum = 0.f, e_S = 0.f, e_q = 0.f, e_Sq = 0.f, e_Sy = 0.f;
-  float e_s2 = 0.f, e_d1 = 0.f, e_e1 = 0.f, e_dz = 0.f;
-  float e_ar[2] = {0.f, 0.f}, e_br[2] = {0.f, 0.f}, e_yr[2] = {0.f, 0.f}, e_wr[2] = {0.f, 0.f}, e_wv[2] = {0.f, 0.f};
-  bool e_isy = false;
-  auto epi = [&](int st, int zs, int64_t yE, float cwE) {
-    if (TR_DUO_SKIP & 4) return;
-    if (st == 0) {
-      e_zp = *reinterpret_cast<const float4*>(sZ + (zs * 16 + c) * 4);
-    } else if (st == 1) {
-      const float zz = cok ? ((e_zp.x + e_zp.y) + e_zp.z) + e_zp.w : NEG;
-      e_x = zz - du_row_max16(zz);
-    } else if (st == 2) {
-      e_ez = cok ? du_exp(e_x) : 0.f;
-      e_sum = du_row_sum16(e_ez);
-    } else if (st == 3) {
-      e_S = e_ez * __builtin_amdgcn_rcpf(e_sum);
-      e_q = cok ? du_exp(e_S) : 0.f;
-      e_isy = cok && (int64_t)c == yE;
-      e_Sq = e_S * e_q;
-      e_Sy = e_isy ? e_S : 0.f;
-    } else if (st == 4) {
-      e_s2 = du_row_sum16(e_q);
-      e_d1 = du_row_sum16(e_Sq);
-      e_e1 = du_row_sum16(e_Sy);
-#pragma unroll
-      for (int rb = 0; rb < 2; ++rb) {
-        e_ar[rb] = du_row_sum16(e_Sq * pcg[rb]);
-        e_br[rb] = du_row_sum16(e_S * pcg[rb]);
-        e_yr[rb] = du_row_sum16(e_Sy * pcg[rb]);
-      }
-    } else if (st == 5) {
-      const float is2 = __builtin_amdgcn_rcpf(e_s2);
-      const float kk = cwE * a.scale;
-      const float dot = kk * (e_d1 * is2 - e_e1);
-      lsum += (wv == 0 && lane == 0) ? (double)cwE * (double)(du_log(e_s2) - e_e1) : 0.0;
-      const float dS = cok ? kk * (e_q * is2 - (e_isy ? 1.0f : 0.0f)) : 0.f;
-      e_dz = cok ? e_S * (dS - dot) : 0.f;
-#pragma unroll
-      for (int rb = 0; rb < 2; ++rb) e_wr[rb] = kk * (e_ar[rb] * is2 - e_yr[rb]) - dot * e_br[rb];
-    } else if (st == 6) {
-#pragma unroll
-      for (int rb = 0; rb < 2; ++rb) {
-        const float w0 = du_rdl(e_wr[rb], 0), w1 = du_rdl(e_wr[rb], 16), w2 = du_rdl(e_wr[rb], 32),
-                    w3 = du_rdl(e_wr[rb], 48);
-        e_wv[rb] = fmaf(w3, sel[3], fmaf(w2, sel[2], fmaf(w1, sel[1], w0 * sel[0])));
-      }
-    } else {
-#pragma unroll
-      for (int rb = 0; rb < 2; ++rb) {
-        gT[rb] += e_wv[rb] * TP[rb];
-        const float ug =
-            fmaf(uP[rb][3], gsel[3], fmaf(uP[rb][2], gsel[2], fmaf(uP[rb][1], gsel[1], uP[rb][0] * gsel[0])));
-        dpc[rb] = fmaf(e_dz, wg[rb] * ug, dpc[rb]);
-      }
-      const float wvV = hv ? e_wv[1] : e_wv[0];
-#pragma unroll
-      for (int qq = 0; qq < 4; ++qq) gV[qq] += wvV * VP[qq];
-    }
-  };
-
-#if TR_DUO_PROFILE
-  unsigned long long prof[4] = {0, 0, 0, 0};
-  unsigned long long prof_t = __builtin_readcyclecounter();
-#endif
-  auto dma_sample = [&](const float* src, int slot) {
-#pragma unroll
-    for (int gi = 0; gi < 8; ++gi)
-      du_dma_s(goff[gi], src, lbase + (uint32_t)(slot * 4 * SPF) + (uint32_t)(wv + DU_NW * gi) * 1024u);
-  };
-  if (nr > 0) {
-    dma_sample(src_of(0), 0);
-    if (PF > 0) du_pf_s(pfoff, src_of(nr > 1 ? 1 : 0), pfm0);
-  }
-  int64_t yN = nr > 0 ? lab[sample_of(0)] : 0;
-
-  auto iter = [&](auto slot_c, int k) {
-    constexpr int SL = decltype(slot_c)::value;
-    const int64_t yC = yN;
-    const bool more = k + 1 < nr;
-    yN = lab[sample_of(more ? k + 1 : k)];
-    if (PF > 0)
-      asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    TR_DUO_MARK(0);
-    du_barrier();
-    TR_DUO_MARK(1);
-    const float cwC = du_rdl(cwl, (int)yC);
-    const float* psrc = (more && !(TR_DUO_SKIP & 1)) ? src_of(k + 1) : src_of(k);
-    const uint32_t pm0 = lbase + (uint32_t)((SL ^ 1) * 4 * SPF) + (uint32_t)wv * 1024u;
-    epi(0, SL ^ 1, yP, cwP);
-    const float* sb = lds + SL * SPF;
-    du_f32x4 aT[2][4], aV[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) aT[0][q] = aT[1][q] = aV[q] = du_f32x4{0.f, 0.f, 0.f, 0.f};
-    // iteration st: V step st (4 MFMAs) and half of T step st >> 1 (rank block st & 1, 4 MFMAs)
-    // (TR_DUO_R8 == 2: every lane reads its whole V quad, lanes c and c ^ 8 the same one; no DPP)
-    constexpr bool VH = TR_DUO_R8 != 2;
-    float4 xt[8], bq[16], xw[16];
-    float2 xv[16];
-    auto ld = [&](int st) {
-      if ((st & 1) == 0) xt[st >> 1] = *reinterpret_cast<const float4*>(sb + aoff[st >> 1]);
-      bq[st] = *reinterpret_cast<const float4*>(sP1 + ((st & 1) ? pb1 : pb0) + 4 * (st >> 1));
-      if (VH)
-        xv[st] = *reinterpret_cast<const float2*>(sb + boff[st & 3] + 4 * J * st);
-      else
-        xw[st] = *reinterpret_cast<const float4*>(sb + boff[st & 3] - 2 * hv + 4 * J * st);
-    };
-#pragma unroll
-    for (int st = 0; st < XL8; ++st) ld(st);
-#pragma unroll
-    for (int st = 0; st < 16; ++st) {
-      if (st + XL8 < 16) ld(st + XL8);
-      if (st % DMA_EVERY == 0 && st / DMA_EVERY < 8)
-        du_dma_s(goff[st / DMA_EVERY], psrc, pm0 + (uint32_t)(st / DMA_EVERY) * 4096u);
-      if (PF > 0 && st == 8) du_pf_s(pfoff, src_of(k + PF < nr ? k + PF : nr - 1), pfm0);
-      const int rb = st & 1;
-      const float4 x = xt[st >> 1];
-      aT[rb][0] = du_mfma(x.x, bq[st].x, aT[rb][0]);
-      aT[rb][1] = du_mfma(x.y, bq[st].y, aT[rb][1]);
-      aT[rb][2] = du_mfma(x.z, bq[st].z, aT[rb][2]);
-      aT[rb][3] = du_mfma(x.w, bq[st].w, aT[rb][3]);
-      float o0, o1, p0, p1;
-      if (VH) {
-        o0 = xv[st].x;
-        o1 = xv[st].y;
-        // row_ror:8: lane c ^ 8's half (every lane valid: no old value)
-        p0 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(o0), 0x128, 0xF, 0xF, true));
-        p1 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(o1), 0x128, 0xF, 0xF, true));
-      } else {  // accumulator k holds element k
-        o0 = xw[st].x;
-        o1 = xw[st].y;
-        p0 = xw[st].z;
-        p1 = xw[st].w;
-      }
-      aV[0] = du_mfma(o0, bopB[st], aV[0]);
-      aV[1] = du_mfma(o1, bopB[st], aV[1]);
-      aV[2] = du_mfma(p0, bopB[st], aV[2]);
-      aV[3] = du_mfma(p1, bopB[st], aV[3]);
-      if ((st & 1) == 1 && st < 15) epi(1 + (st >> 1), SL ^ 1, yP, cwP);
-      if (SB) __builtin_amdgcn_sched_barrier(0);
-    }
-    TR_DUO_MARK(2);
-    float u[2];
-#pragma unroll
-    for (int rb = 0; rb < 2; ++rb) {
-      const du_f32x4 T = (aT[rb][0] + aT[rb][1]) + (aT[rb][2] + aT[rb][3]);
-      TP[rb] = T;
-      float x = phiU[rb][0] * T.x;
-      x = fmaf(phiU[rb][1], T.y, x);
-      x = fmaf(phiU[rb][2], T.z, x);
-      x = fmaf(phiU[rb][3], T.w, x);
-      u[rb] = x;
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) VP[q] = aV[q];
-#pragma unroll
-    for (int rb = 0; rb < 2; ++rb) {
-      float x = u[rb];
-      x += du_dpp<0x124>(x);  // row_ror:4
-      x += du_dpp<0x128>(x);  // row_ror:8
-      x = du_xor16_sum(x);
-      x = du_xor32_sum(x);
-      u[rb] = x;
-    }
-#pragma unroll
-    for (int rb = 0; rb < 2; ++rb)
-#pragma unroll
-      for (int n = 0; n < 4; ++n) uP[rb][n] = du_rdl(u[rb], n);
-    float zpart = wpc[0] * uP[0][0];
-#pragma unroll
-    for (int r = 1; r < 8; ++r) zpart = fmaf(wpc[r], uP[r >> 2][r & 3], zpart);
-    sZ[(SL * 16 + c) * 4 + wv] = zpart;  // every row the same value
-    yP = yC;
-    cwP = cwC;
-    TR_DUO_MARK(3);
-  };
-  for (int k = 0; k < nr; k += 2) {
-    iter(std::integral_constant<int, 0>(), k);
-    if (k + 1 < nr) iter(std::integral_constant<int, 1>(), k + 1);
-  }
-#if TR_DUO_PROFILE
-  if (lane == 0 && blockIdx.x < 512)
-    for (int q = 0; q < 4; ++q) g_duo_prof[blockIdx.x][wv][q] = prof[q];
-#endif
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  du_barrier();
-  if (nr > 0) {
-#pragma unroll
-    for (int st = 0; st < 8; ++st) epi(st, (nr - 1) & 1, yP, cwP);
-  }
-
-  // ---- fixed-order reduction into an LDS image of the arena (wave order), slab ----
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      float x = gV[q][v];
-      x += __shfl_xor(x, 16, TR_WAVE);
-      x += __shfl_xor(x, 32, TR_WAVE);
-      gV[q][v] = x;
-    }
-  float* sG = lds + g.du_oG;
-  __syncthreads();
-  for (int64_t e = t; e < g.slab; e += DU_T) sG[e] = 0.f;
-  __syncthreads();
-  for (int ws = 0; ws < DU_NW; ++ws) {
-    if (ws == wv) {
-#pragma unroll
-      for (int rb = 0; rb < 2; ++rb) {
-        const int r = 4 * rb + l3;
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          const int row = 64 * ib + 4 * (lane >> 2) + v;
-          if (r < R) sG[row * R + r] += gT[rb][v];
-        }
-        const int rg = 4 * rb + grow;
-        if (cok && rg < R) sG[g.offPC + c * R + rg] += dpc[rb];
-      }
-      if (lane < 16 && rv < R) {
-        // accumulator q, register m: column 32 jq + 16 ((c >> 2) & 1) + 4 m + (q ^ 2 hv), rank rv
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-#pragma unroll
-          for (int m = 0; m < 4; ++m) {
-            const int j = 32 * jq + 16 * ((c >> 2) & 1) + 4 * m + (TR_DUO_R8 != 2 ? q ^ (2 * hv) : q);
-            sG[g.offP1 + j * R + rv] += gV[q][m];
-          }
-      }
-    }
-    __syncthreads();
-  }
-  if (wv == 0) {
-    lsum = tr_wave_allreduce_d(lsum);
-    if (lane == 0) {
-      a.dpart[2 * blockIdx.x] = lsum;
-      a.dpart[2 * blockIdx.x + 1] = 0.0;
-    }
-  }
-  float* slab = a.gpart + (int64_t)blockIdx.x * g.slab;
-  for (int64_t e = t; e < g.slab; e += DU_T) slab[e] = sG[e];
-}
-
 template <int JT>
 __global__ __launch_bounds__(DU_T, 2) void k_mnl_duo(MnlGeom g, DuArgs a, const int64_t* __restrict__ lab,
                                                   const float* __restrict__ class_w, const int32_t* __restrict__ stop) {
@@ -920,10 +546,7 @@ __global__ __launch_bounds__(DU_T, 2) void k_mnl_duo(MnlGeom g, DuArgs a, const 
   if (stop != nullptr && *stop != 0) return;
   const int lane = threadIdx.x & (TR_WAVE - 1);
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / TR_WAVE);
-  if constexpr (TR_DUO_R8)
-    duo8_body<JT>(g, a, lab, class_w, lds, wv, lane);
-  else
-    duo_body<JT>(g, a, lab, class_w, lds, wv, lane);
+  duo_body<JT>(g, a, lab, class_w, lds, wv, lane);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -3,9 +3,19 @@
 
 Same module functions and `CP_linear_regression` class (same arguments, defaults, attributes,
 factor layouts Bcp_n (I, Rn, 1) and Bcp_c (W, Rs, n_complex_dim+1), (D, Rs, 1), (n_out, Rs, 1),
-`loss_running` semantics), with the fit/predict hot path on gfx950: both W-side factors are
-contracted in one MFMA GEMM per sample with X_n staged in LDS, and the backward GEMM reuses the
-staged sample, so X is read from HBM once per iteration (tensor_regression_amd/csrc/tr_spectral.hip).
+`loss_running` semantics), with the fit/predict hot path on gfx950, each sample of X read from
+HBM once per iteration.  Kernel envelope (the plan picks the first that covers the shape):
+  * training at config-5-like shapes — X.shape[1] == 256, 97 <= X.shape[2] <= 130 (a multiple
+    of 4 below 128), rank_normal <= 16, rank_spectral * (n_complex_dim + 1) <= 16,
+    n_complex_dim + 1 in {1, 2, 4}, n_out <= 64 — runs the column-slice single pass
+    k_spec_slice (csrc/tr_spectral_slice.hip: bf16 split GEMMs on the matrix cores);
+  * other shapes with K = rank_normal + rank_spectral * (n_complex_dim + 1) <= 32,
+    X.shape[1], X.shape[2], n_out <= 256 and the whole sample in a CU's 160 KiB LDS (and every
+    predict / predict_latents call of such shapes) run the whole-sample single pass k_spec_fused
+    (csrc/tr_spectral.hip);
+  * the rest, up to K <= 256 with one sample's epilogue (X.shape[2] * (K + 1) +
+    (X.shape[2] + n_out) * (rank_normal + rank_spectral) floats) in a CU's LDS, the three-kernel
+    path (csrc/tr_spectral_gen.hip).  Outside that the plan raises ValueError.
 
 Reference semantics kept as they are: the fit model is
 lin_model + stepwise_spectral_model (norm BEFORE the d/out contractions) while predict uses
@@ -13,11 +23,7 @@ lin_model + spectral_model (norm AFTER the full contraction); the bias is added 
 the spectral fit_Adam / fit stop on a NaN loss.
 
 Deliberate differences: tensors run on a HIP device, fp32 only; a y with n_out == 1 is
-rejected (the reference broadcasts (N,) + (N,1) to (N,N), Q10).  Shapes within X.shape[1],
-X.shape[2], n_out <= 256 and K = rank_normal + rank_spectral*(n_complex_dim+1) <= 32 run the
-single-pass kernel (csrc/tr_spectral.hip); larger ones the three-kernel path
-(csrc/tr_spectral_gen.hip) up to K <= 256 and one sample's epilogue (X.shape[2]*(K+1) +
-(X.shape[2]+n_out)*(rank_normal+rank_spectral) floats) within a CU's 160 KiB LDS.
+rejected (the reference broadcasts (N,) + (N,1) to (N,N), Q10).
 """
 import numpy as np
 import torch

@@ -203,3 +203,44 @@ def test_gradient_allreduce_falls_back_to_torch_for_gloo():
         assert torch.equal(t, torch.arange(5, dtype=torch.float32))
     finally:
         dist.destroy_process_group()
+
+
+class _FakeClock:
+    def __init__(self):
+        self.t = 0.0
+
+    def __call__(self):
+        return self.t
+
+    def sleep(self, dt):
+        self.t += 1.0  # every poll advances one "second"
+
+
+class _FakeEvent:
+    """completes once the fake clock reaches `at`"""
+
+    def __init__(self, clock, at):
+        self.clock, self.at = clock, at
+
+    def query(self):
+        return self.clock.t >= self.at
+
+
+def test_watchdog_counts_time_without_progress():
+    """A healthy but slow chunk (64 all-reduces, 10 s apart: 640 s in all) passes a 30 s
+    watchdog, because every completed all-reduce restarts the clock (the bound used
+    to cover the whole chunk); a stall of more than 30 s after the 5th all-reduce trips it."""
+    from tensor_regression_amd._engine import wait_progress, _CollectiveTimeout, _CollectiveError
+    clk = _FakeClock()
+    evs = [_FakeEvent(clk, 10.0 * (k + 1)) for k in range(64)]
+    wait_progress(evs, lambda: None, 30.0, clock=clk, sleep=clk.sleep)
+    assert clk.t >= 640.0
+    clk = _FakeClock()
+    evs = [_FakeEvent(clk, 10.0 * (k + 1)) for k in range(5)] + [_FakeEvent(clk, 1e9)]
+    with pytest.raises(_CollectiveTimeout, match="5 of the 6"):
+        wait_progress(evs, lambda: None, 30.0, clock=clk, sleep=clk.sleep)
+    assert 80.0 <= clk.t <= 82.0
+    clk = _FakeClock()
+    errs = iter([None, None, "remote process exited"])
+    with pytest.raises(_CollectiveError, match="remote process"):
+        wait_progress([_FakeEvent(clk, 1e9)], lambda: next(errs), 1e6, clock=clk, sleep=clk.sleep)
