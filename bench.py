@@ -522,7 +522,7 @@ def main():
             torch.distributed.barrier()
 
     comm = None
-    if pg is not None and world > 1:
+    if pg is not None:  # (world 1 too with TR_BENCH_FORCE_PG=1: the RCCL path on one GPU)
         from tensor_regression_amd import _engine
         comm = _engine.gradient_allreduce(pg, local)
         if isinstance(comm, _engine.RcclAllReduce):
@@ -610,7 +610,7 @@ def main():
         dom_all = [float(p[1]) for p in parts]
         rows_all = [int(p[2]) for p in parts]
         el = max(el_all)
-        if world > 1:
+        if world > 1 or comm is not None:
             ranks_block = rank_summary(world, rows_all, el_all, dom_all, args.steps,
                                        comm.count() if comm is not None else None, ar_samples,
                                        plan.num_grads * 4, args.scaling)

@@ -102,7 +102,8 @@ hipError_t launch_reduce_slabs(int W, const float* part, int64_t nslabs, int64_t
                                const float* chain_dphi = nullptr, float* chain_out = nullptr, int64_t nchain = 0,
                                const uint32_t* err = nullptr);
 hipError_t launch_mttkrp(const FactorSet& fs, const float* phi, const float* dphi, const float* w,
-                         const float* G, float* grad, const int32_t* stop, hipStream_t st);
+                         const float* G, float* grad, const int32_t* stop, hipStream_t st, float* part = nullptr,
+                         int64_t part_cap = 0);
 hipError_t launch_update(const FactorSet& fs, int n_bias, float* params, const float* grad,
                          const UpdateArgs& ua, float* m, float* v, float* vmax, float* grad_total_out,
                          float* loss_out, double* loss_hist, int32_t* stop, hipStream_t st,
@@ -114,6 +115,9 @@ hipError_t launch_converge(const double* loss_hist, int64_t hist_base, int64_t i
 bool update_prepare_mode_ok(const FactorSet& fs, int mode);
 // MTTKRP of a two-factor model, one wave per factor row (tr_update.hip); launch_mttkrp uses it
 bool mttkrp2_supported(const FactorSet& fs);
+bool mttkrp3_supported(const FactorSet& fs, int64_t part_cap);
+hipError_t launch_mttkrp3(const FactorSet& fs, const float* phi, const float* dphi, const float* w, const float* G,
+                          float* grad, float* part, int64_t part_cap, const int32_t* stop, hipStream_t st);
 hipError_t launch_mttkrp2(const FactorSet& fs, const float* phi, const float* dphi, const float* w, const float* G,
                           float* grad, const int32_t* stop, hipStream_t st);
 

@@ -15,6 +15,8 @@
 // Every reduction is a fixed-order tree (wave butterfly, then LDS in wave order, then slabs
 // in index order) so a run is bitwise reproducible; no float atomics anywhere.
 
+#include <cstdlib>
+
 #include "tr_common.h"
 #include "tr_kernels.h"
 
@@ -1397,8 +1399,13 @@ static hipError_t mttkrp_launch_r(const FactorSet& fs, const float* phi, const f
 }
 
 hipError_t launch_mttkrp(const FactorSet& fs, const float* phi, const float* dphi, const float* w,
-                         const float* G, float* grad, const int32_t* stop, hipStream_t st) {
+                         const float* G, float* grad, const int32_t* stop, hipStream_t st, float* part,
+                         int64_t part_cap) {
   if (mttkrp2_supported(fs)) return launch_mttkrp2(fs, phi, dphi, w, G, grad, stop, st);
+  const char* m3e = std::getenv("TR_MTTKRP3");  // 0: the general k_mttkrp for three factors too
+  const bool m3 = m3e == nullptr || m3e[0] != '0';
+  if (m3 && part != nullptr && mttkrp3_supported(fs, part_cap))
+    return launch_mttkrp3(fs, phi, dphi, w, G, grad, part, part_cap, stop, st);
   int64_t rows = 0;
   for (int f = 0; f < fs.nf; ++f) rows += fs.dim[f];
   const int64_t padded = rows * (fs.rank | 1);  // odd LDS row stride (k_mttkrp)

@@ -41,6 +41,10 @@ struct MnlGeom {
   // one (i, j) block; LDS carve of ONE workgroup (floats)
   int duo;
   int du_oZ, du_oP1, du_oG, du_oPF, du_lds_floats;
+  // bf16-split form of the two-workgroups-per-CU kernel (k_mnl_bsp, the default where it fits:
+  // a 32 KiB (128, 64) or (64, 128) sample, R <= 8, C <= 16; TR_DUO_SPLIT=0 keeps the rank-block
+  // form): U partials at bs_oU
+  int bsp, bs_oU;
 };
 
 // Fills g; false (with a reason) when the shape is outside the kernel's envelope.

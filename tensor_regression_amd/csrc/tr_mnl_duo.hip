@@ -13,6 +13,13 @@
 // over a 2-sample ring (2 x 32 KiB), and TWO workgroups share a CU: while one workgroup sits in
 // its barrier or its latency-bound epilogue, the other's MFMAs run on the same SIMDs.
 //
+// What bounds it (round 5): the sample stream.  The timing ablations of round 4 kept the LDS-DMA
+// instructions (the "no DMA" build refilled the same, L2-resident sample) and so pointed at the
+// instruction stream; with the DMA removed entirely the bf16-split body below runs in 0.256 ms at
+// config 3 against 0.368 ms with it.  The non-temporal policy on the sample pieces (TR_DUO_NT, as
+// k_mnl_fused and k_linear_fused use) takes 6-7 % off both bodies (rank-block 0.364 -> 0.339 ms);
+// a second sample in flight per workgroup (TR_DUO_2IF) does not help.
+//
 // Per sample k of a workgroup: wait own LDS-DMA of k -> barrier -> epilogue of k-1 (Z partials
 // of the 2 A-waves, double softmax, Wv, gradient scaling) -> GEMM of k with the DMA of k+1 into
 // the other ring slot interleaved.  The A-waves read Phi1 (their B operand) from a transposed
@@ -53,7 +60,8 @@ __device__ unsigned long long g_duo_prof[512][4][4];
                         // step, read-ahead 3 / 3 steps to fit 256 registers (the (128, 64) shape only)
 #endif
 #ifndef TR_DUO_SKIP
-#define TR_DUO_SKIP 0  // profiling ablation only (results invalid): 1 loop LDS-DMA, 2 MFMAs, 4 epilogue
+#define TR_DUO_SKIP 0  // profiling ablation only (results invalid): 1 loop LDS-DMA, 2 MFMAs, 4 epilogue;
+                       // bsp form: 8 no LDS-DMA at all after the first sample, 16 no label loads
 #endif
 
 namespace tr {
@@ -100,7 +108,12 @@ constexpr bool IL = TR_DUO_IL != 0;
 // of k (one dword LDS-DMA into a scratch line per wave), so the LDS-DMA of that sample one
 // iteration later meets L2 / MALL latency instead of a loaded HBM round trip; 0: no prefetch
 constexpr int PF = TR_DUO_PF;
-constexpr int DU_GMAX = 12;  // LDS-DMA pieces (1 KiB) per wave per sample (sample <= 48 KiB)
+#ifndef TR_DUO_2IF
+#define TR_DUO_2IF 0
+#endif
+// bsp form: 1 = two samples in flight per workgroup (sample k + 2 into slot k & 1 once every wave
+// holds its operands of k: a second barrier per sample); 0 = one (k + 1 into the other slot)
+constexpr bool TIF = TR_DUO_2IF != 0;
 typedef float du_f32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ du_f32x4 du_mfma(float a, float b, du_f32x4 c) {
@@ -153,6 +166,41 @@ __device__ __forceinline__ void du_dma16(const float* gsrc, const float* lds_dst
                : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(a))
                : "memory");
 }
+// ---- bf16 split helpers (the bsp form below; same pieces as tr_spectral_slice.hip) ----
+typedef __bf16 bs_bf8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bs_bf2 __attribute__((ext_vector_type(2)));
+typedef uint32_t sl_u4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ du_f32x4 bs_mfma(sl_u4 a, const uint32_t (&b)[4], du_f32x4 c) {
+  if (TR_DUO_SKIP & 2) return c + __uint_as_float(a[0]) * __uint_as_float(b[0]);
+  const sl_u4 bb = sl_u4{b[0], b[1], b[2], b[3]};
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bs_bf8, a), __builtin_bit_cast(bs_bf8, bb), c, 0,
+                                                 0, 0);
+}
+// two values -> one VGPR of packed round-to-nearest-even bf16 (element 0 = a), v_cvt_pk_bf16_f32
+__device__ __forceinline__ uint32_t sl_pack_rne(float a, float b) {
+  return __builtin_bit_cast(uint32_t, bs_bf2{(__bf16)a, (__bf16)b});
+}
+typedef _Float16 bs_h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 bs_h2 __attribute__((ext_vector_type(2)));
+// two values -> one VGPR of packed round-to-nearest-even f16, v_cvt_pk_f16_f32
+__device__ __forceinline__ uint32_t bs_pack_h(float a, float b) {
+  return __builtin_bit_cast(uint32_t, bs_h2{(_Float16)a, (_Float16)b});
+}
+__device__ __forceinline__ du_f32x4 bs_mfma_h(sl_u4 a, const uint32_t (&b)[4], du_f32x4 c) {
+  if (TR_DUO_SKIP & 2) return c + __uint_as_float(a[0]) * __uint_as_float(b[0]);
+  const sl_u4 bb = sl_u4{b[0], b[1], b[2], b[3]};
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(bs_h8, a), __builtin_bit_cast(bs_h8, bb), c, 0, 0,
+                                                0);
+}
+__device__ __forceinline__ float sl_lo_f32(uint32_t h) { return __uint_as_float(__builtin_amdgcn_perm(h, h, 0x01000c0cu)); }
+__device__ __forceinline__ float sl_hi_f32(uint32_t h) { return __uint_as_float(h & 0xffff0000u); }
+// a (element 2m), b (element 2m + 1) -> three packed round-to-nearest pieces: x = x1 + x2 + x3 exactly
+__device__ __forceinline__ void sl_split2(float a, float b, uint32_t& h1, uint32_t& h2, uint32_t& h3) {
+  h1 = sl_pack_rne(a, b);
+  const float ra = a - sl_lo_f32(h1), rb = b - sl_hi_f32(h1);
+  h2 = sl_pack_rne(ra, rb);
+  h3 = sl_pack_rne(ra - sl_lo_f32(h2), rb - sl_hi_f32(h2));
+}
 }  // namespace
 
 struct DuArgs {
@@ -180,9 +228,17 @@ __device__ __forceinline__ void du_pf_s(uint32_t voff, const float* sbase, uint3
 // One LDS-DMA piece per lane with a scalar base: 16 B from sbase + voff (bytes, per lane) to LDS
 // byte address m0v + 16 * lane.  No per-piece 64-bit address arithmetic; m0 is compiler-reserved
 // and is saved / restored inside the statement.
+#ifndef TR_DUO_NT
+#define TR_DUO_NT 1  // non-temporal policy on the sample LDS-DMA (bsp at c3: 0.341 vs 0.364 ms)
+#endif
+#if TR_DUO_NT
+#define DU_NT " nt"
+#else
+#define DU_NT ""
+#endif
 __device__ __forceinline__ void du_dma_s(uint32_t voff, const float* sbase, uint32_t m0v) {
   uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" DU_NT "\n\ts_mov_b32 m0, %0"
                : "=&s"(keep)
                : "v"(voff), "s"(sbase), "s"(m0v)
                : "memory");
@@ -539,6 +595,386 @@ __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, cons
   for (int64_t e = t; e < g.slab; e += DU_T) slab[e] = sG[e];
 }
 
+// ------------------------------------------------------------------------------------------
+// bf16-split form (g.bsp, the default where it fits): the same per-sample math on
+// v_mfma_f32_16x16x32_bf16 with the fp32 operands split into round-to-nearest bf16 pieces, as
+// the spectral slice kernel does (tr_spectral_slice.hip "bf16 split"): X in two pieces
+// (|x - x1 - x2| < 2^-16 |x|, unbiased), the factors in three, and the rank columns packed so
+// that one 16-wide MFMA carries every piece product of weight >= 2^-17:
+//   B12 = [b1 | b2] (columns 0-7 | 8-15, rank = column & 7), B3 = [b3 | 0]
+//   acc += x1.B12 + x2.B12 + x1.B3  ->  column r + column r + 8 = x1b1 + x1b2 + x2b1 + x2b2 + x1b3
+// A sample (I x J = 8192 floats) takes 96 MFMAs per workgroup instead of 512 4x4x1 ones: the
+// rank-block form spends 1,024 issue cycles per wave-sample on MFMAs alone.  Work of wave wv:
+//   T[i, r] over i-tiles of 16 rows (J = 64: tiles 2 wv, 2 wv + 1; J = 128: tile wv) and every
+//     32-deep j k-step: A = X rows (two ds_read_b128 of consecutive chunks per lane)
+//   V[j, r] over 4 j-tiles for ONE 32-deep i k-step (J = 64: k-step wv; J = 128: k-step wv & 1,
+//     chunk group wv >> 1): j-tile t holds j = 4 c + t for chunk c = lane row, so one ds_read_b128
+//     of chunk c of row i gives element i of four tiles (eight reads: the k-step's 32 i)
+// The chunk swizzle q ^ (i & 15) makes both reads conflict-free.  T is complete per wave (its
+// U partial over its rows goes through LDS: four partials per sample); V is a partial over the
+// wave's i k-step, and dPhi1 = sum_n Wv_n V_n is linear in it: the waves' partials are summed
+// once, at the end.  Every wave runs the softmax epilogue of the previous sample (staged between
+// its GEMM steps) for all 8 ranks; wave 0 alone accumulates dPhiC and the loss.
+template <int JT>
+__device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, const int64_t* __restrict__ lab,
+                                         const float* __restrict__ class_w, float* lds, const int wv, const int lane) {
+  const int t = threadIdx.x;
+  constexpr int J = JT, I = 8192 / JT, SPF = 8192, JQ = J / 4;
+  constexpr int NT = I / 64;   // T i-tiles per wave
+  constexpr int NKT = J / 32;  // T k-steps (j)
+  const int R = g.R, C = g.C;
+  float* sU = lds + g.bs_oU;  // [2 parity][4 waves][8 ranks] U partials
+  const float* P0 = a.phi;
+  const float* P1 = a.phi + g.offP1;
+  const float* PC = a.phi + g.offPC;
+  const int n = lane & 15, gq = lane >> 4, r8 = n & 7;
+  const bool lo8 = n < 8, rok = r8 < R;
+  const int c = n;  // epilogue: class lane c, DPP row gq (ranks gq and gq + 4)
+  const bool cok = c < C;
+  const float cwl = cok ? class_w[c] : 0.f;
+  const float NEG = -__builtin_huge_valf();
+  float gsel[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) gsel[q] = gq == q ? 1.f : 0.f;
+  float rsel[8];  // 1 where this lane's accumulator rank (n & 7) == r
+#pragma unroll
+  for (int r = 0; r < 8; ++r) rsel[r] = r8 == r ? 1.f : 0.f;
+
+  const int it0 = NT == 2 ? 32 * wv : 16 * wv;                    // first T row of this wave
+  const int iv0 = I == 128 ? 32 * wv : 32 * (wv & 1);             // V k-step (rows) of this wave
+  const int cv = n + (J == 128 ? 16 * (wv >> 1) : 0);             // V chunk (j = 4 cv + tile)
+  // B operands, split once per launch: T (Phi1, element e of lane group gq <-> j = 32 s + 8 gq + e)
+  uint32_t bT12[NKT][4], bT3[NKT][4], hT[NKT][4], bV12[4], bV3[4], hV[4];
+  auto bsplit = [&](float x0, float x1, uint32_t& b12, uint32_t& b3, uint32_t& hh) {
+    uint32_t h1, h2, h3;
+    sl_split2(x0, x1, h1, h2, h3);
+    b12 = lo8 ? h1 : h2;
+    b3 = lo8 ? h3 : 0u;
+    // f16 pieces for the sample's second piece: [f16(x) | f16(x - f16(x))]
+    const uint32_t f1 = bs_pack_h(x0, x1);
+    const bs_h2 f1v = __builtin_bit_cast(bs_h2, f1);
+    const uint32_t f2 = bs_pack_h(x0 - (float)f1v[0], x1 - (float)f1v[1]);
+    hh = lo8 ? f1 : f2;
+  };
+#pragma unroll
+  for (int s = 0; s < NKT; ++s)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int j = 32 * s + 8 * gq + 2 * v;
+      bsplit(rok ? P1[(int64_t)j * R + r8] : 0.f, rok ? P1[(int64_t)(j + 1) * R + r8] : 0.f, bT12[s][v], bT3[s][v],
+             hT[s][v]);
+    }
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {  // V (Phi0, element e <-> i = iv0 + 8 gq + e)
+    const int i = iv0 + 8 * gq + 2 * v;
+    bsplit(rok ? P0[(int64_t)i * R + r8] : 0.f, rok ? P0[(int64_t)(i + 1) * R + r8] : 0.f, bV12[v], bV3[v], hV[v]);
+  }
+  // U weights: T accumulator (lane (n, gq), reg v) = T[it0 + 16 tt + 4 gq + v][n & 7] after the
+  // column fold; lanes n >= 8 hold the same values and weigh 0
+  float phiU[NT][4];
+#pragma unroll
+  for (int tt = 0; tt < NT; ++tt)
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+      phiU[tt][v] = (lo8 && rok) ? P0[(int64_t)(it0 + 16 * tt + 4 * gq + v) * R + r8] : 0.f;
+  // epilogue weights: pc[r] = w_r PhiC[c][r]; row gq's ranks gq, gq + 4
+  float pc[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) pc[r] = (cok && r < R) ? a.w[r] * PC[c * R + r] : 0.f;
+  const float pcg0 = pc[gq & 3], pcg1 = pc[4 + (gq & 3)];
+  const float wg0 = gq < R ? a.w[gq] : 0.f, wg1 = gq + 4 < R ? a.w[gq + 4] : 0.f;
+  for (int e = t; e < 2 * 4 * 8; e += DU_T) sU[e] = 0.f;
+
+  // LDS-DMA map (as the rank-block form): wave wv issues the 1 KiB groups wv + 4 gi of every sample
+  uint32_t goff[8];
+#pragma unroll
+  for (int gi = 0; gi < 8; ++gi) {
+    const int slot = (wv + DU_NW * gi) * TR_WAVE + lane;
+    const int i = slot / JQ;
+    const int q = slot - i * JQ;
+    goff[gi] = 4u * (uint32_t)(i * J + 4 * (q ^ (i & 15)));
+  }
+  const uint32_t lbase = (uint32_t)__builtin_amdgcn_readfirstlane(
+      (int)(uint32_t)(uintptr_t)((const __attribute__((address_space(3))) float*)lds));
+  // LDS read offsets (floats): T row it0 + 16 tt + n, chunks 8 s + 2 gq (+1); V rows iv0 + 8 gq + e, chunk cv
+  int tro[NT], vro[8];
+#pragma unroll
+  for (int tt = 0; tt < NT; ++tt) tro[tt] = (it0 + 16 * tt + n) * J;
+  const int tsw = n;  // (it0 + 16 tt + n) & 15 = n
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int i = iv0 + 8 * gq + e;
+    vro[e] = i * J + 4 * (cv ^ (i & 15));
+  }
+
+  const int64_t n0 = (int64_t)blockIdx.x * a.rows_per_wg;
+  const int64_t n1 = n0 + a.rows_per_wg < a.N ? n0 + a.rows_per_wg : a.N;
+  const int nr = (int)(n1 > n0 ? n1 - n0 : 0);
+  auto sample_of = [&](int k) -> int64_t { return n0 + (a.reverse ? (nr - 1 - k) : k); };
+  auto src_of = [&](int k) -> const float* { return a.X + sample_of(k) * a.xld; };
+
+  __syncthreads();
+  __builtin_amdgcn_s_waitcnt(0);
+
+  du_f32x4 gT[NT], gV[4];  // dPhi0 rows of this wave's T tiles, dPhi1 partial of its V tiles
+#pragma unroll
+  for (int q = 0; q < NT; ++q) gT[q] = du_f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) gV[q] = du_f32x4{0.f, 0.f, 0.f, 0.f};
+  float dpc0 = 0.f, dpc1 = 0.f;  // wave 0: dPhiC[c][gq], dPhiC[c][gq + 4]
+  double lsum = 0.0;
+  du_f32x4 TP[NT], VP[4];  // the previous sample's T and V (folded), for its epilogue
+#pragma unroll
+  for (int q = 0; q < NT; ++q) TP[q] = du_f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) VP[q] = du_f32x4{0.f, 0.f, 0.f, 0.f};
+  int64_t yP = 0;
+  float cwP = 0.f;
+
+  // ---- epilogue of one sample in 8 stages (duo_body's chain, all 8 ranks: row gq carries ranks
+  // gq and gq + 4) ----
+  float uS = 0.f, uR[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) uR[r] = 0.f;
+  float e_x = 0.f, e_ez = 0.f, e_sum = 0.f, e_S = 0.f, e_q = 0.f, e_Sq = 0.f, e_Sy = 0.f;
+  float e_s2 = 0.f, e_d1 = 0.f, e_e1 = 0.f, e_dz = 0.f, e_a0 = 0.f, e_b0 = 0.f, e_y0 = 0.f, e_a1 = 0.f, e_b1 = 0.f,
+        e_y1 = 0.f, e_w0 = 0.f, e_w1 = 0.f, e_wv = 0.f;
+  bool e_isy = false;
+  auto epi = [&](int st, int zs, int64_t yE, float cwE) {
+    if (TR_DUO_SKIP & 4) return;
+    if (st == 0) {  // U[r] = sum of the four waves' partials (lane r), wave order
+      const float* pu = sU + zs * 32 + r8;
+      uS = ((pu[0] + pu[8]) + pu[16]) + pu[24];
+    } else if (st == 1) {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) uR[r] = du_rdl(uS, r);
+      float zz = pc[0] * uR[0];
+#pragma unroll
+      for (int r = 1; r < 8; ++r) zz = fmaf(pc[r], uR[r], zz);
+      zz = cok ? zz : NEG;
+      e_x = zz - du_row_max16(zz);
+    } else if (st == 2) {
+      e_ez = cok ? du_exp(e_x) : 0.f;
+      e_sum = du_row_sum16(e_ez);
+    } else if (st == 3) {
+      e_S = e_ez * __builtin_amdgcn_rcpf(e_sum);
+      e_q = cok ? du_exp(e_S) : 0.f;
+      e_isy = cok && (int64_t)c == yE;
+      e_Sq = e_S * e_q;
+      e_Sy = e_isy ? e_S : 0.f;
+    } else if (st == 4) {
+      e_s2 = du_row_sum16(e_q);
+      e_d1 = du_row_sum16(e_Sq);
+      e_e1 = du_row_sum16(e_Sy);
+      e_a0 = du_row_sum16(e_Sq * pcg0);
+      e_b0 = du_row_sum16(e_S * pcg0);
+      e_y0 = du_row_sum16(e_Sy * pcg0);
+      e_a1 = du_row_sum16(e_Sq * pcg1);
+      e_b1 = du_row_sum16(e_S * pcg1);
+      e_y1 = du_row_sum16(e_Sy * pcg1);
+    } else if (st == 5) {
+      const float is2 = __builtin_amdgcn_rcpf(e_s2);
+      const float kk = cwE * a.scale;
+      const float dot = kk * (e_d1 * is2 - e_e1);
+      lsum += (wv == 0 && lane == 0) ? (double)cwE * (double)(du_log(e_s2) - e_e1) : 0.0;
+      const float dS = cok ? kk * (e_q * is2 - (e_isy ? 1.0f : 0.0f)) : 0.f;
+      e_dz = cok ? e_S * (dS - dot) : 0.f;
+      e_w0 = kk * (e_a0 * is2 - e_y0) - dot * e_b0;  // Wv[gq]
+      e_w1 = kk * (e_a1 * is2 - e_y1) - dot * e_b1;  // Wv[gq + 4]
+    } else if (st == 6) {
+      // Wv[r] of this lane's accumulator rank r = n & 7 (rank r < 4: row r's e_w0, else row r - 4's e_w1)
+      float wv8 = 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        wv8 = fmaf(du_rdl(e_w0, 16 * r), rsel[r], wv8);
+        wv8 = fmaf(du_rdl(e_w1, 16 * r), rsel[r + 4], wv8);
+      }
+      e_wv = wv8;
+    } else {
+#pragma unroll
+      for (int q = 0; q < NT; ++q) gT[q] += e_wv * TP[q];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) gV[q] += e_wv * VP[q];
+      if (wv == 0) {  // dPhiC[c][r] += dZ[c] w_r U[r], r = gq, gq + 4
+        const float u0 = fmaf(uR[3], gsel[3], fmaf(uR[2], gsel[2], fmaf(uR[1], gsel[1], uR[0] * gsel[0])));
+        const float u1 = fmaf(uR[7], gsel[3], fmaf(uR[6], gsel[2], fmaf(uR[5], gsel[1], uR[4] * gsel[0])));
+        dpc0 = fmaf(e_dz, wg0 * u0, dpc0);
+        dpc1 = fmaf(e_dz, wg1 * u1, dpc1);
+      }
+    }
+  };
+
+  auto dma_sample = [&](const float* src, int slot) {
+#pragma unroll
+    for (int gi = 0; gi < 8; ++gi)
+      du_dma_s(goff[gi], src, lbase + (uint32_t)(slot * 4 * SPF) + (uint32_t)(wv + DU_NW * gi) * 1024u);
+  };
+  // two samples in flight per workgroup: sample k + 2 goes into slot k & 1 as soon as every wave
+  // holds its operands of k in registers (a second barrier per sample); the kernel is bound by the
+  // bytes in flight per CU, not by its issue stream (no-LDS-DMA ablation: 0.256 vs 0.368 ms at c3)
+  if (nr > 0) dma_sample(src_of(0), 0);
+  if (nr > 0 && TIF) dma_sample(src_of(nr > 1 ? 1 : 0), 1);
+  int64_t yN = nr > 0 ? lab[sample_of(0)] : 0;
+#if TR_DUO_PROFILE
+  unsigned long long prof[4] = {0, 0, 0, 0};
+  unsigned long long prof_t = __builtin_readcyclecounter();
+#endif
+
+  auto iter = [&](auto slot_c, int k) {
+    constexpr int SL = decltype(slot_c)::value;
+    const int64_t yC = yN;
+    const bool more = k + 1 < nr;
+    if (!(TR_DUO_SKIP & 16)) yN = lab[sample_of(more ? k + 1 : k)];
+    if (TIF)
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // own pieces of k (those of k + 1 may be in flight)
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    TR_DUO_MARK(0);
+    du_barrier();  // everyone's pieces of k; U partials of k - 1
+    TR_DUO_MARK(1);
+    const float cwC = du_rdl(cwl, (int)yC);
+    // sample k + 2 into this slot once it is read (past the end: a harmless refill of a valid sample)
+    const int kd = TIF ? k + 2 : k + 1;  // the sample this iteration's DMA brings in
+    const float* psrc = (kd < nr && !(TR_DUO_SKIP & 1)) ? src_of(kd) : src_of(nr - 1);
+    const uint32_t pm0 = lbase + (uint32_t)((TIF ? SL : SL ^ 1) * 4 * SPF) + (uint32_t)wv * 1024u;
+    epi(0, SL ^ 1, yP, cwP);
+    const float* sb = lds + SL * SPF;
+    du_f32x4 aT[NT], aV[4];
+#pragma unroll
+    for (int q = 0; q < NT; ++q) aT[q] = du_f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) aV[q] = du_f32x4{0.f, 0.f, 0.f, 0.f};
+    // every operand of sample k into registers, then the slot is released (second barrier)
+    constexpr int NU = NT * NKT;  // T steps (4); then 4 V steps (one j-tile each)
+    du_f32x4 xv[8], xt[NU][2];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) xv[e] = *reinterpret_cast<const du_f32x4*>(sb + vro[e]);
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int tt = u / NKT, s = u - tt * NKT;
+      const int q0 = 8 * s + 2 * gq;
+      xt[u][0] = *reinterpret_cast<const du_f32x4*>(sb + tro[tt] + 4 * (q0 ^ tsw));
+      xt[u][1] = *reinterpret_cast<const du_f32x4*>(sb + tro[tt] + 4 * ((q0 + 1) ^ tsw));
+    }
+    if (TIF) du_barrier();  // (its lgkmcnt(0): this wave's reads landed) every wave's operands of k read
+#pragma unroll
+    for (int st = 0; st < NU + 4; ++st) {
+      if (!(TR_DUO_SKIP & 8)) du_dma_s(goff[st], psrc, pm0 + (uint32_t)st * 4096u);
+      sl_u4 x1, x2;
+      if (st < NU) {
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const du_f32x4& xr = xt[st][v >> 1];
+          const float e0 = xr[2 * (v & 1)], e1 = xr[2 * (v & 1) + 1];
+          const uint32_t h = sl_pack_rne(e0, e1);
+          x1[v] = h;
+          x2[v] = bs_pack_h(e0 - sl_lo_f32(h), e1 - sl_hi_f32(h));
+        }
+        const int tt = st / NKT, s = st - tt * NKT;
+        aT[tt] = bs_mfma_h(x2, hT[s], aT[tt]);
+        aT[tt] = bs_mfma(x1, bT3[s], aT[tt]);
+        aT[tt] = bs_mfma(x1, bT12[s], aT[tt]);
+      } else {
+        const int tv = st - NU;  // j-tile: element tv of each row's chunk
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const float e0 = xv[2 * v][tv], e1 = xv[2 * v + 1][tv];
+          const uint32_t h = sl_pack_rne(e0, e1);
+          x1[v] = h;
+          x2[v] = bs_pack_h(e0 - sl_lo_f32(h), e1 - sl_hi_f32(h));
+        }
+        aV[tv] = bs_mfma_h(x2, hV, aV[tv]);
+        aV[tv] = bs_mfma(x1, bV3, aV[tv]);
+        aV[tv] = bs_mfma(x1, bV12, aV[tv]);
+      }
+      if (st >= 1 && st <= 7) epi(st, SL ^ 1, yP, cwP);
+      if (SB) __builtin_amdgcn_sched_barrier(0);
+    }
+    TR_DUO_MARK(2);
+    // fold the piece columns (rank r = column r + column r + 8), U partial of this wave -> LDS
+    float u = 0.f;
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) {
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        aT[tt][v] += du_dpp<0x128>(aT[tt][v]);  // row_ror:8
+        u = fmaf(phiU[tt][v], aT[tt][v], u);
+      }
+      TP[tt] = aT[tt];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+#pragma unroll
+      for (int v = 0; v < 4; ++v) aV[q][v] += du_dpp<0x128>(aV[q][v]);
+      VP[q] = aV[q];
+    }
+    u = du_xor32_sum(du_xor16_sum(u));  // lane (n < 8, any row): this wave's U partial of rank n
+    if (lane < 8) sU[SL * 32 + wv * 8 + lane] = u;
+    yP = yC;
+    cwP = cwC;
+    TR_DUO_MARK(3);
+  };
+  for (int k = 0; k < nr; k += 2) {
+    iter(std::integral_constant<int, 0>(), k);
+    if (k + 1 < nr) iter(std::integral_constant<int, 1>(), k + 1);
+  }
+#if TR_DUO_PROFILE
+  if (lane == 0 && blockIdx.x < 512)
+    for (int q = 0; q < 4; ++q) g_duo_prof[blockIdx.x][wv][q] = prof[q];
+#endif
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last (harmless) refill has landed
+  du_barrier();  // U partials of the last sample
+  if (nr > 0) {
+#pragma unroll
+    for (int st = 0; st < 8; ++st) epi(st, (nr - 1) & 1, yP, cwP);
+  }
+
+  // ---- fixed-order reduction into an LDS image of the arena (wave order), slab ----
+  float* sG = lds + g.du_oG;
+  __syncthreads();
+  for (int64_t e = t; e < g.slab; e += DU_T) sG[e] = 0.f;
+  __syncthreads();
+  for (int ws = 0; ws < DU_NW; ++ws) {
+    if (ws == wv && lo8 && rok) {
+#pragma unroll
+      for (int tt = 0; tt < NT; ++tt)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) sG[(it0 + 16 * tt + 4 * gq + v) * R + r8] += gT[tt][v];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int j = 4 * (cv - n + 4 * gq + v) + q;  // chunk (row 4 gq + v of the tile) -> j = 4 chunk + tile
+          sG[g.offP1 + j * R + r8] += gV[q][v];
+        }
+    }
+    if (ws == wv && wv == 0 && cok) {
+      if (gq < R) sG[g.offPC + c * R + gq] += dpc0;
+      if (gq + 4 < R) sG[g.offPC + c * R + gq + 4] += dpc1;
+    }
+    __syncthreads();
+  }
+  if (wv == 0) {
+    lsum = tr_wave_allreduce_d(lsum);
+    if (lane == 0) {
+      a.dpart[2 * blockIdx.x] = lsum;
+      a.dpart[2 * blockIdx.x + 1] = 0.0;
+    }
+  }
+  float* slab = a.gpart + (int64_t)blockIdx.x * g.slab;
+  for (int64_t e = t; e < g.slab; e += DU_T) slab[e] = sG[e];
+}
+
+template <int JT>
+__global__ __launch_bounds__(DU_T, 2) void k_mnl_bsp(MnlGeom g, DuArgs a, const int64_t* __restrict__ lab,
+                                                  const float* __restrict__ class_w, const int32_t* __restrict__ stop) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  if (stop != nullptr && *stop != 0) return;
+  const int lane = threadIdx.x & (TR_WAVE - 1);
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / TR_WAVE);
+  bsp_body<JT>(g, a, lab, class_w, lds, wv, lane);
+}
+
 template <int JT>
 __global__ __launch_bounds__(DU_T, 2) void k_mnl_duo(MnlGeom g, DuArgs a, const int64_t* __restrict__ lab,
                                                   const float* __restrict__ class_w, const int32_t* __restrict__ stop) {
@@ -553,17 +989,29 @@ __global__ __launch_bounds__(DU_T, 2) void k_mnl_duo(MnlGeom g, DuArgs a, const 
 // host side
 // ------------------------------------------------------------------------------------------
 static const void* duo_kernel(const MnlGeom& g) {
+  if (g.bsp)
+    return g.J == 64 ? reinterpret_cast<const void*>(&k_mnl_bsp<64>) : reinterpret_cast<const void*>(&k_mnl_bsp<128>);
   return g.J == 64 ? reinterpret_cast<const void*>(&k_mnl_duo<64>) : reinterpret_cast<const void*>(&k_mnl_duo<128>);
 }
 
 void mnl_duo_geom(MnlGeom* g) {
   g->duo = 0;
+  g->bsp = 0;
   const char* env = std::getenv("TR_MNL_DUO");
   if (env != nullptr && env[0] == '0') return;
   // compiled shapes: a 32 KiB sample as (128, 64) or (64, 128) (two 64-row blocks, 8 LDS-DMA
   // groups per wave, chunk swizzle q ^ (i & 15))
-  if (!g->full || g->I * g->J != 8192 || (g->J != 64 && g->J != 128) || g->nrb != 2 || g->C > kMnlCMax) return;
+  if (!g->full || g->I * g->J != 8192 || (g->J != 64 && g->J != 128) || g->C > kMnlCMax) return;
   if (g->smask != 15) return;
+  // form: the f32 rank-block body where it fits (R in 5..8: two rank blocks), the bf16-split body
+  // for R <= 4; TR_DUO_SPLIT=1 takes the split body for R <= 8, =0 the rank-block body only.
+  // (With the non-temporal sample DMA both run at the same rate at c3 — 0.339 / 0.343-0.347 ms,
+  // the sample stream bounds them — and the rank-block form is the more accurate: 3.1e-7 vs
+  // 7.2e-7 normwise from fp64 at full c3 size, the reference's own fp32 7.8e-7.)
+  const char* spl = std::getenv("TR_DUO_SPLIT");
+  const bool force_split = spl != nullptr && spl[0] == '1', no_split = spl != nullptr && spl[0] == '0';
+  const bool bsp = g->R <= 8 && !no_split && (force_split || g->nrb != 2);
+  if (!bsp && g->nrb != 2) return;
   const int64_t spf = (int64_t)g->I * g->J;
   int64_t o = 2 * spf;  // ring of two samples
   g->du_oZ = (int)o;
@@ -573,18 +1021,20 @@ void mnl_duo_geom(MnlGeom* g) {
   o = (o + 3) & ~(int64_t)3;
   g->du_oPF = (int)o;  // prefetch scratch line (64 dwords, written by every wave, never read)
   o += TR_WAVE;
+  g->bs_oU = (int)o;  // bsp: [2][4 waves][8 ranks] U partials
+  o += 2 * 4 * 8;
   g->du_oG = g->slab <= 2 * spf ? 0 : (int)o;  // the arena image aliases the drained ring
   if (g->du_oG) o += g->slab;
   o = (o + 3) & ~(int64_t)3;
   if (2 * o * 4 > 160 * 1024) return;  // two workgroups per CU
   g->du_lds_floats = (int)o;
   g->duo = 1;
+  g->bsp = bsp ? 1 : 0;
 }
 
-hipError_t mnl_duo_prepare(MnlGeom* g) {
-  if (!g->duo) return hipSuccess;
-  const void* k = duo_kernel(*g);
-  const size_t lds = (size_t)g->du_lds_floats * 4;
+static hipError_t duo_kernel_ok(const MnlGeom& g, bool* ok) {
+  const void* k = duo_kernel(g);
+  const size_t lds = (size_t)g.du_lds_floats * 4;
   hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   hipFuncAttributes attr;
@@ -593,7 +1043,24 @@ hipError_t mnl_duo_prepare(MnlGeom* g) {
   int nb = 0;
   e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, DU_T, lds);
   if (e != hipSuccess) return e;
-  if (attr.localSizeBytes > 0 || nb < 2) g->duo = 0;  // spills or not two per CU: k_mnl_fused
+  *ok = attr.localSizeBytes == 0 && nb >= 2;  // no spills, two per CU
+  return hipSuccess;
+}
+
+hipError_t mnl_duo_prepare(MnlGeom* g) {
+  if (!g->duo) return hipSuccess;
+  bool ok = false;
+  hipError_t e = duo_kernel_ok(*g, &ok);
+  if (e != hipSuccess) return e;
+  if (ok) return hipSuccess;
+  if (g->bsp && g->nrb == 2) {  // the rank-block form instead
+    g->bsp = 0;
+    e = duo_kernel_ok(*g, &ok);
+    if (e != hipSuccess) return e;
+    if (ok) return hipSuccess;
+  }
+  g->duo = 0;  // k_mnl_fused
+  g->bsp = 0;
   return hipSuccess;
 }
 
@@ -603,10 +1070,16 @@ hipError_t launch_mnl_duo(const MnlGeom& g, int grid, const float* X, int64_t N,
   if (grid < 1 || rows_per_wg < 0 || xld % 4 != 0 || (int64_t)grid * rows_per_wg < N) return hipErrorInvalidValue;
   DuArgs a{X, N, xld, phi, w, scale, gpart, dpart, rows_per_wg, reverse};
   const size_t lds = (size_t)g.du_lds_floats * 4;
-if (g.J == 64)
+  if (g.bsp) {
+    if (g.J == 64)
+      hipLaunchKernelGGL((k_mnl_bsp<64>), dim3(grid), dim3(DU_T), lds, st, g, a, lab, class_w, stop);
+    else
+      hipLaunchKernelGGL((k_mnl_bsp<128>), dim3(grid), dim3(DU_T), lds, st, g, a, lab, class_w, stop);
+  } else if (g.J == 64) {
     hipLaunchKernelGGL((k_mnl_duo<64>), dim3(grid), dim3(DU_T), lds, st, g, a, lab, class_w, stop);
-  else
+  } else {
     hipLaunchKernelGGL((k_mnl_duo<128>), dim3(grid), dim3(DU_T), lds, st, g, a, lab, class_w, stop);
+  }
   return hipGetLastError();
 }
 

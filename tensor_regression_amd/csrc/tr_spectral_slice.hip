@@ -319,7 +319,7 @@ __device__ __forceinline__ uint32_t sl_lds_addr(const float* p) {
 __device__ __forceinline__ void sl_dma16bq(__amdgpu_buffer_rsrc_t rs, uint32_t tstr, uint32_t q, uint32_t voff,
                                            uint32_t lds_b, uint32_t lds_off) {
   uint32_t keep, so;
-  asm volatile("s_mul_i32 %1, %4, %5\n\ts_mov_b32 %0, m0\n\ts_add_u32 m0, %3, %7\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %6, %1 offen lds" SL_NT "\n\ts_mov_b32 m0, %0"
+  asm volatile("s_mul_i32 %1, %4, %5\n\ts_mov_b32 %0, m0\n\ts_add_u32 m0, %3, %7\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %6, %1 offen" SL_NT " lds\n\ts_mov_b32 m0, %0"
                : "=&s"(keep), "=&s"(so)
                : "v"(voff), "s"(lds_b), "s"(tstr), "s"(q), "s"(rs), "s"(lds_off)
                : "memory", "scc");
@@ -348,14 +348,14 @@ __device__ __forceinline__ void sl_dma16(const float* gsrc, const float* lds_dst
 // the descriptor's range reads 0
 __device__ __forceinline__ void sl_dma4b(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t lds_b) {
   uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen lds" SL_NT "\n\ts_mov_b32 m0, %0"
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen" SL_NT " lds\n\ts_mov_b32 m0, %0"
                : "=&s"(keep)
                : "v"(voff), "s"(rs), "s"(lds_b)
                : "memory");
 }
 __device__ __forceinline__ void sl_dma16b(__amdgpu_buffer_rsrc_t rs, uint32_t soff, uint32_t voff, uint32_t lds_b) {
   uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds" SL_NT "\n\ts_mov_b32 m0, %0"
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen" SL_NT " lds\n\ts_mov_b32 m0, %0"
                : "=&s"(keep)
                : "v"(voff), "s"(rs), "s"(lds_b), "s"(soff)
                : "memory");

@@ -330,6 +330,171 @@ hipError_t launch_mttkrp2(const FactorSet& fs, const float* phi, const float* dp
 }
 
 
+// ==========================================================================================
+// MTTKRP of a three-factor model as two small GEMM stages (config 4: dims 64 x 64 x 32, rank 16;
+// the autograd of cp_to_tensor, standard…py:123-130).  Modes by dense stride: s (slowest), m,
+// q (stride 1), G = the dense gradient, a_f = w (.) Phi_f rows:
+//   dA_s[i, r] = w_r sum_j a_m[j, r] H[i, j, r]        H[i, j, r] = sum_k G[i, j, k] Phi_q[k, r]
+//   dA_m[j, r] = w_r sum_i Phi_s[i, r] H[i, j, r]
+//   dA_q[k, r] = w_r sum_{i, j} G[i, j, k] Phi_s[i, r] Phi_m[j, r]
+// k_mttkrp3_part: one workgroup per (i, block of JB rows j): its G block (JB x I_q floats,
+// contiguous) is read once, coalesced, into LDS; H_block = G_block . Phi_q (a (JB x I_q) x
+// (I_q x R) GEMM) and G_block^T . (Phi_m (.) Phi_s[i]) (an (I_q x JB) x (JB x R) GEMM) give its
+// partials of all three gradients.  k_mttkrp3_sum adds the partials in a fixed order and applies
+// the softplus chain.  (k_mttkrp, tr_kernels.hip, walks each factor row's slice of G: the
+// stride-1 mode's rows read G at a 128-B stride, every line of G once per row: 24.5 us at c4.)
+// ==========================================================================================
+namespace {
+constexpr int M3_T = 256;
+constexpr int M3_TILE = 4096;  // floats of G per workgroup at most
+constexpr int M3_FQR = 8192;   // I_q * R floats of Phi_q in LDS at most
+}  // namespace
+
+struct Mttkrp3Geom {
+  int fs_, fm, fq;  // factor index of the slow / middle / fast mode
+  int Is, Im, Iq, JB, NJ, R, slab;
+};
+
+static bool mttkrp3_geom(const FactorSet& fs, Mttkrp3Geom* g) {
+  if (fs.nf != 3 || fs.rank < 1 || fs.rank > 16) return false;
+  int ord[3] = {0, 1, 2};
+  for (int a = 0; a < 3; ++a)
+    for (int b = a + 1; b < 3; ++b)
+      if (fs.stride[ord[b]] > fs.stride[ord[a]]) {
+        const int t = ord[a];
+        ord[a] = ord[b];
+        ord[b] = t;
+      }
+  // a dense row-major layout under the permutation (stride-1 fast mode, no gaps)
+  if (fs.stride[ord[2]] != 1 || fs.stride[ord[1]] != fs.dim[ord[2]] ||
+      fs.stride[ord[0]] != fs.dim[ord[1]] * fs.dim[ord[2]])
+    return false;
+  g->fs_ = ord[0];
+  g->fm = ord[1];
+  g->fq = ord[2];
+  g->Is = (int)fs.dim[ord[0]];
+  g->Im = (int)fs.dim[ord[1]];
+  g->Iq = (int)fs.dim[ord[2]];
+  g->R = fs.rank;
+  if (g->Iq > M3_TILE || (int64_t)g->Iq * g->R > M3_FQR) return false;
+  g->JB = M3_TILE / g->Iq;
+  if (g->JB > g->Im) g->JB = g->Im;
+  if (g->JB > 32) g->JB = 32;  // c4: 2 blocks per row i, 128 workgroups
+  g->NJ = (g->Im + g->JB - 1) / g->JB;
+  g->slab = g->R * (1 + g->JB + g->Iq);
+  return true;
+}
+
+__global__ __launch_bounds__(M3_T) void k_mttkrp3_part(FactorSet fs, Mttkrp3Geom g, const float* __restrict__ phi,
+                                                       const float* __restrict__ G, float* __restrict__ part,
+                                                       const int32_t* __restrict__ stop) {
+  if (stop != nullptr && *stop != 0) return;
+  __shared__ __attribute__((aligned(16))) float sG[M3_TILE];
+  __shared__ float sQ[M3_FQR];    // Phi_q [k][r]
+  __shared__ float sM[64 * 16];   // Phi_m rows of the block [j][r] times Phi_s[i, r]
+  __shared__ float sH[64 * 16];   // H[j][r]
+  __shared__ float sS[16];
+  const int t = threadIdx.x, R = g.R, Iq = g.Iq;
+  const int i = blockIdx.x / g.NJ, jb = blockIdx.x - i * g.NJ;
+  const int j0 = jb * g.JB, nj = g.Im - j0 < g.JB ? g.Im - j0 : g.JB;
+  const float* __restrict__ Ps = phi + fs.off[g.fs_];
+  const float* __restrict__ Pm = phi + fs.off[g.fm];
+  const float* __restrict__ Pq = phi + fs.off[g.fq];
+  // the block's G rows: nj * Iq contiguous floats
+  const float* __restrict__ Gb = G + ((int64_t)i * g.Im + j0) * Iq;
+  const int ng = nj * Iq;
+  if ((((uintptr_t)Gb) & 15) == 0 && (ng & 3) == 0) {
+    for (int e = 4 * t; e < ng; e += 4 * M3_T)
+      *reinterpret_cast<float4*>(sG + e) = *reinterpret_cast<const float4*>(Gb + e);
+  } else {
+    for (int e = t; e < ng; e += M3_T) sG[e] = Gb[e];
+  }
+  for (int e = t; e < Iq * R; e += M3_T) sQ[e] = Pq[e];
+  if (t < R) sS[t] = Ps[(int64_t)i * R + t];
+  __syncthreads();
+  for (int e = t; e < nj * R; e += M3_T) {
+    const int r = e % R;
+    sM[e] = Pm[(int64_t)(j0 + e / R) * R + r] * sS[r];
+  }
+  // H[j][r] = sum_k G[j][k] Phi_q[k][r]   (nj x R outputs)
+  for (int e = t; e < nj * R; e += M3_T) {
+    const int j = e / R, r = e - j * R;
+    const float* gr = sG + j * Iq;
+    float h = 0.f;
+    for (int k = 0; k < Iq; ++k) h = fmaf(gr[k], sQ[k * R + r], h);
+    sH[e] = h;
+  }
+  __syncthreads();
+  float* slab = part + (int64_t)blockIdx.x * g.slab;
+  // slab: [ s-partial (R) | m-partials (JB x R) | q-partials (Iq x R) ]
+  if (t < R) {  // sum_j H[j][r] Phi_m[j][r] (times Phi_s only in the m partial)
+    float a = 0.f;
+    for (int j = 0; j < nj; ++j) a = fmaf(sH[j * R + t], Pm[(int64_t)(j0 + j) * R + t], a);
+    slab[t] = a;
+  }
+  for (int e = t; e < nj * R; e += M3_T) slab[R + e] = sH[e] * sS[e % R];
+  // q partial[k][r] = sum_j G[j][k] Phi_m[j][r] Phi_s[i][r]
+  for (int e = t; e < Iq * R; e += M3_T) {
+    const int k = e / R, r = e - k * R;
+    float a = 0.f;
+    for (int j = 0; j < nj; ++j) a = fmaf(sG[j * Iq + k], sM[j * R + r], a);
+    slab[R + g.JB * R + e] = a;
+  }
+}
+
+__global__ __launch_bounds__(M3_T) void k_mttkrp3_sum(FactorSet fs, Mttkrp3Geom g, const float* __restrict__ dphi,
+                                                      const float* __restrict__ w, const float* __restrict__ part,
+                                                      float* __restrict__ out, const int32_t* __restrict__ stop) {
+  if (stop != nullptr && *stop != 0) return;
+  const int R = g.R;
+  const int64_t e = (int64_t)blockIdx.x * M3_T + threadIdx.x;
+  const int64_t ns = (int64_t)g.Is * R, nm = (int64_t)g.Im * R, nq = (int64_t)g.Iq * R;
+  if (e >= ns + nm + nq) return;
+  float acc = 0.f;
+  int f;
+  int64_t row;
+  int r;
+  if (e < ns) {  // dA_s[i][r]: the NJ blocks of row i
+    f = g.fs_;
+    row = e / R;
+    r = (int)(e - row * R);
+    for (int jb = 0; jb < g.NJ; ++jb) acc += part[(row * g.NJ + jb) * g.slab + r];
+  } else if (e < ns + nm) {  // dA_m[j][r]: every i of j's block
+    f = g.fm;
+    const int64_t x = e - ns;
+    row = x / R;
+    r = (int)(x - row * R);
+    const int jb = (int)(row / g.JB), jj = (int)(row - (int64_t)jb * g.JB);
+    for (int i = 0; i < g.Is; ++i) acc += part[((int64_t)i * g.NJ + jb) * g.slab + R + jj * R + r];
+  } else {  // dA_q[k][r]: every block
+    f = g.fq;
+    const int64_t x = e - ns - nm;
+    row = x / R;
+    r = (int)(x - row * R);
+    const int64_t nb = (int64_t)g.Is * g.NJ;
+    for (int64_t b = 0; b < nb; ++b) acc += part[b * g.slab + R + (int64_t)g.JB * R + x];
+  }
+  const int64_t o = fs.off[f] + row * R + r;
+  out[o] = acc * w[r] * dphi[o];
+}
+
+bool mttkrp3_supported(const FactorSet& fs, int64_t part_cap) {
+  Mttkrp3Geom g;
+  if (!mttkrp3_geom(fs, &g)) return false;
+  return (int64_t)g.Is * g.NJ * g.slab <= part_cap;
+}
+
+hipError_t launch_mttkrp3(const FactorSet& fs, const float* phi, const float* dphi, const float* w, const float* G,
+                          float* grad, float* part, int64_t part_cap, const int32_t* stop, hipStream_t st) {
+  Mttkrp3Geom g;
+  if (!mttkrp3_geom(fs, &g) || (int64_t)g.Is * g.NJ * g.slab > part_cap) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_mttkrp3_part, dim3((unsigned)(g.Is * g.NJ)), dim3(M3_T), 0, st, fs, g, phi, G, part, stop);
+  const int64_t nout = (int64_t)(g.Is + g.Im + g.Iq) * g.R;
+  hipLaunchKernelGGL(k_mttkrp3_sum, dim3((unsigned)((nout + M3_T - 1) / M3_T)), dim3(M3_T), 0, st, fs, g, dphi, w,
+                     part, grad, stop);
+  return hipGetLastError();
+}
+
 bool update_prepare_mode_ok(const FactorSet& fs, int mode) {
   // mode 1: phi / dphi of the new factors, elementwise.  (Building dense B in the update too was
   // measured slower than the separate multi-workgroup k_build_dense: one CU took 17 us for

@@ -192,4 +192,12 @@ def test_world2_fit_matches_single_process(world2, case, capsys):
     assert len(facs) == len(r0["factors"])
     for a, b in zip(r0["factors"], facs):
         assert a.shape == b.shape
+        if a.numel() == 1:
+            # the bias: it crosses zero during the fit (final value ~ -0.006 after 20 steps of
+            # lr 0.01), and Adam normalises each coordinate's step by its own gradient scale, so
+            # fp32 summation-order noise of a near-zero gradient moves it by a fraction of a step:
+            # held to RTOL of the path length lr * ITERS instead of RTOL of its final value
+            d = abs(float(a.reshape(-1)[0]) - float(np.asarray(b).reshape(-1)[0]))
+            assert d <= RTOL * max(abs(float(np.asarray(b).reshape(-1)[0])), 0.01 * ITERS), (case, d)
+            continue
         assert normwise_rel(a.numpy(), b) <= RTOL, (case, a.shape, normwise_rel(a.numpy(), b))

@@ -35,9 +35,12 @@ def path(kind):
     (force the two-pass kernels: linear rows/cols, multinomial MFMA forward + cols), 'valu'
     (multinomial: two-pass with the VALU forward) or 'spi1' (multinomial single pass with one
     sample per barrier instead of pairs) or 'noduo' (multinomial single pass with one 8-wave
-    workgroup per CU instead of the two-workgroups-per-CU variant)."""
+    workgroup per CU instead of the two-workgroups-per-CU variant) or 'split' (the
+    two-workgroups-per-CU variant in its bf16-split form, TR_DUO_SPLIT=1, instead of its default
+    f32 rank-block form; the split form is the default only for rank <= 4)."""
     from tensor_regression_amd import standard_tensor_regression as S
-    saved = {k: os.environ.get(k) for k in ("TR_FORCE_TWOPASS", "TR_NO_MFMA", "TR_MNL_SPI", "TR_MNL_DUO")}
+    saved = {k: os.environ.get(k) for k in ("TR_FORCE_TWOPASS", "TR_NO_MFMA", "TR_MNL_SPI", "TR_MNL_DUO",
+                                            "TR_DUO_SPLIT")}
     for k in saved:
         os.environ.pop(k, None)
     if kind == "twopass":
@@ -50,6 +53,8 @@ def path(kind):
         os.environ["TR_MNL_DUO"] = "0"
     if kind == "noduo":
         os.environ["TR_MNL_DUO"] = "0"
+    if kind == "split":
+        os.environ["TR_DUO_SPLIT"] = "1"
     S._plan_cache.clear()
     try:
         yield
@@ -146,7 +151,7 @@ def test_linear_golden(name, kind):
             _assert_factors(model.Bcp, d["Bcp_final2_list"])
 
 
-@pytest.mark.parametrize("kind", ["auto", "noduo", "spi1", "twopass", "valu"])
+@pytest.mark.parametrize("kind", ["auto", "split", "noduo", "spi1", "twopass", "valu"])
 @pytest.mark.parametrize("name", MNL)
 def test_multinomial_golden(name, kind):
     with path(kind):
@@ -188,7 +193,8 @@ def _multinomial_golden(name, kind="auto"):
     if name.startswith("mnl_duo"):
         # the fixtures at config 3's sample shapes pin the kernel config 3 runs (k_mnl_duo: its
         # epilogue uses the hardware exp2/log2 units, so it is pinned separately from k_mnl_fused)
-        want = {"auto": " duo ", "noduo": "mnl-fused-1pass", "spi1": "mnl-fused-1pass"}.get(kind, "2pass")
+        want = {"auto": "form=rankblock", "split": "form=bf16split", "noduo": "mnl-fused-1pass",
+                "spi1": "mnl-fused-1pass"}.get(kind, "2pass")
         assert want in plan.describe, plan.describe
         if kind in ("noduo", "spi1"):
             assert " duo " not in plan.describe, plan.describe
@@ -376,7 +382,7 @@ MNL_SHAPES = [((50, 8, 4), 2, 2), ((200, 16, 8), 10, 4), ((97, 5, 7), 16, 3), ((
               ((120, 6, 5), 5, 70), ((80, 4, 8), 20, 130)]
 
 
-@pytest.mark.parametrize("kind", ["auto", "noduo", "spi1", "twopass", "valu"])
+@pytest.mark.parametrize("kind", ["auto", "split", "noduo", "spi1", "twopass", "valu"])
 @pytest.mark.parametrize("shape,C,rank", MNL_SHAPES)
 def test_multinomial_sweep_vs_oracle(shape, C, rank, kind):
     with path(kind):
@@ -801,3 +807,31 @@ def test_kernel_timing_records_and_sampling():
     assert lr0 == lr1 == lr5
     for a, b, c in zip(f0, f1, f5):
         assert torch.equal(a, b) and torch.equal(a, c)
+
+
+@pytest.mark.parametrize("shape,rank", [((16384, 64, 64, 32), 16), ((300, 7, 5, 33), 5), ((200, 9, 130, 3), 16),
+                                        ((64, 20, 3, 50), 1), ((90, 4, 33, 17), 7)])
+def test_mttkrp3_matches_general_kernel(shape, rank, monkeypatch):
+    """The three-factor MTTKRP as two GEMM stages (k_mttkrp3_part / _sum, csrc/tr_update.hip)
+    against the general k_mttkrp (TR_MTTKRP3=0) on the same plan and dense gradient: the same
+    factor gradients up to summation order (config-4 shard first)."""
+    from tensor_regression_amd import CP_linear_regression
+    g = torch.Generator(device=DEV).manual_seed(7)
+    X = torch.randn(*shape, device=DEV, generator=g)
+    y = torch.randn(shape[0], device=DEV, generator=g)
+    torch.manual_seed(3)
+    model = CP_linear_regression(X.shape, rank=rank, non_negative=[False, True, False], device=DEV)
+    plan = model._get_plan(X, shape[0])
+    arena = plan.pack(model.Bcp, model.bias)
+    outs = {}
+    for m3 in ("1", "0"):
+        monkeypatch.setenv("TR_MTTKRP3", m3)
+        grad = torch.zeros(plan.num_grads, device=DEV)
+        gtot = torch.zeros(plan.num_params, device=DEV)
+        loss = torch.zeros(1, device=DEV)
+        plan.loss_grad(X, y, None, float(shape[0]), arena, model.weights, grad)
+        plan.finalize_grad(arena, grad, 0.01, gtot, loss)
+        outs[m3] = [v.cpu().numpy().astype(np.float64) for v in plan.factor_views(gtot)]
+    errs = [float(np.linalg.norm(a - b) / np.linalg.norm(b)) for a, b in zip(outs["1"], outs["0"])]
+    print(shape, rank, plan.describe, errs)
+    assert max(errs) <= (1e-7 if shape[0] == 16384 else 1e-6), errs
