@@ -442,6 +442,20 @@ __global__ __launch_bounds__(M3_T) void k_mttkrp3_part(FactorSet fs, Mttkrp3Geom
   }
 }
 
+// sum of n values at a stride in a fixed order: eight interleaved running sums, combined by a
+// fixed tree (a single running sum over the 128 block partials of config 4 doubled the fast
+// factor's distance from fp64 against k_mttkrp's per-row butterfly)
+__device__ __forceinline__ float m3_sum(const float* __restrict__ p, int64_t stride, int n) {
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int b = 0;
+  for (; b + 8 <= n; b += 8) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a[u] += p[(int64_t)(b + u) * stride];
+  }
+  for (int u = 0; b + u < n; ++u) a[u] += p[(int64_t)(b + u) * stride];
+  return ((a[0] + a[4]) + (a[2] + a[6])) + ((a[1] + a[5]) + (a[3] + a[7]));
+}
+
 __global__ __launch_bounds__(M3_T) void k_mttkrp3_sum(FactorSet fs, Mttkrp3Geom g, const float* __restrict__ dphi,
                                                       const float* __restrict__ w, const float* __restrict__ part,
                                                       float* __restrict__ out, const int32_t* __restrict__ stop) {
@@ -458,21 +472,20 @@ __global__ __launch_bounds__(M3_T) void k_mttkrp3_sum(FactorSet fs, Mttkrp3Geom 
     f = g.fs_;
     row = e / R;
     r = (int)(e - row * R);
-    for (int jb = 0; jb < g.NJ; ++jb) acc += part[(row * g.NJ + jb) * g.slab + r];
+    acc = m3_sum(part + row * g.NJ * g.slab + r, g.slab, g.NJ);
   } else if (e < ns + nm) {  // dA_m[j][r]: every i of j's block
     f = g.fm;
     const int64_t x = e - ns;
     row = x / R;
     r = (int)(x - row * R);
     const int jb = (int)(row / g.JB), jj = (int)(row - (int64_t)jb * g.JB);
-    for (int i = 0; i < g.Is; ++i) acc += part[((int64_t)i * g.NJ + jb) * g.slab + R + jj * R + r];
+    acc = m3_sum(part + (int64_t)jb * g.slab + R + jj * R + r, (int64_t)g.NJ * g.slab, g.Is);
   } else {  // dA_q[k][r]: every block
     f = g.fq;
     const int64_t x = e - ns - nm;
     row = x / R;
     r = (int)(x - row * R);
-    const int64_t nb = (int64_t)g.Is * g.NJ;
-    for (int64_t b = 0; b < nb; ++b) acc += part[b * g.slab + R + (int64_t)g.JB * R + x];
+    acc = m3_sum(part + R + (int64_t)g.JB * R + x, g.slab, g.Is * g.NJ);
   }
   const int64_t o = fs.off[f] + row * R + r;
   out[o] = acc * w[r] * dphi[o];

@@ -239,3 +239,54 @@ def test_split_errors_alone_stay_far_below_the_bar():
     (test_gpu_fullsize.py::test_spectral_full_size_bar_rejects_truncating_split)."""
     e_def, e_tr = _full_size_grad_errs()
     assert e_def < 1e-6 / 10 and e_tr < 1e-6 / 10, (e_def, e_tr)
+
+
+def split_bf16_f16(x):
+    """The multinomial duo kernel's bf16-split body (k_mnl_bsp, tr_mnl_duo.hip): x1 = bf16_rne(x),
+    x2 = f16_rne(x - x1) (v_cvt_pk_bf16_f32 / v_cvt_pk_f16_f32)"""
+    x = np.asarray(x, dtype=np.float32)
+    x1 = rne_bf16(x)
+    x2 = (x - x1).astype(np.float32).astype(np.float16)
+    return x1, x2
+
+
+def test_bf16_f16_split_bound():
+    """x1 + x2 represents x to 2^-20 |x| for 2^-5 <= |x| < 2^24: |x - x1| <= 2^-8 |x| (half a bf16
+    ulp), and its f16 rounding keeps 11 significant bits (2^-12 relative) while it is a normal f16,
+    or an absolute 2^-25 (half the subnormal spacing) below — 2^-20 |x| again at |x| >= 2^-5;
+    below 2^-5 the error stays <= 2^-25 absolute.  Median 2^-22.5 (measured here)."""
+    g = np.random.default_rng(8)
+    x = (g.standard_normal(400000) * np.exp2(g.integers(-12, 24, 400000))).astype(np.float32)
+    x1, x2 = split_bf16_f16(x)
+    assert np.all(np.isfinite(x2.astype(np.float64)))
+    err = np.abs(x.astype(np.float64) - x1.astype(np.float64) - x2.astype(np.float64))
+    ax = np.abs(x.astype(np.float64))
+    big = ax >= 2.0 ** -5
+    assert np.all(err[big] <= ax[big] * 2.0 ** -20)
+    assert np.all(err[~big] <= 2.0 ** -25)
+    assert np.median(err[big] / ax[big]) < 2.0 ** -22
+    # versus two bf16 pieces (the spectral kernel's X): 2^-17 / 2^-19.5 worst / median here,
+    # 8x / 7x coarser
+    x2b = rne_bf16((x - x1).astype(np.float32))
+    errb = np.abs(x.astype(np.float64) - x1.astype(np.float64) - x2b.astype(np.float64))
+    assert np.median(errb[big] / ax[big]) > 6 * np.median(err[big] / ax[big])
+    assert (errb[big] / ax[big]).max() > 6 * (err[big] / ax[big]).max()
+
+
+def test_bsp_products_cover_every_term():
+    """One 16-wide accumulator per tile: x1.[b1 | b2] + x1.[b3 | 0] (bf16) + x2.[h1 | h2] (f16,
+    h1 = f16(b), h2 = f16(b - h1)), columns r and r + 8 folded: x1 (b1 + b2 + b3) + x2 (h1 + h2),
+    i.e. x1 b exactly plus x2 b to 2^-22: the product's error is the representation error of x"""
+    a, b = _rand(20000, 9), _rand(20000, 10)
+    m = min(len(a), len(b))
+    a, b = a[:m], b[:m]
+    ok = (np.abs(a) > 2.0 ** -5) & (np.abs(a) < 2.0 ** 20) & (np.abs(b) > 2.0 ** -10) & (np.abs(b) < 2.0 ** 14)
+    a, b = a[ok], b[ok]
+    x1, x2 = (p.astype(np.float64) for p in split_bf16_f16(a))
+    b1, b2, b3 = (p.astype(np.float64) for p in split3(b))
+    h1 = b.astype(np.float16)
+    h2 = (b - h1.astype(np.float32)).astype(np.float16)
+    prod = x1 * (b1 + b2 + b3) + x2 * (h1.astype(np.float64) + h2.astype(np.float64))
+    exact = a.astype(np.float64) * b.astype(np.float64)
+    rel = np.abs(prod - exact) / np.abs(exact)
+    assert rel.max() <= 2.0 ** -19.9
