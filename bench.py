@@ -626,7 +626,10 @@ def main():
         try:
             with open(args.traffic) as f:
                 tj = json.load(f)
-            ent = tj.get(args.config, {}).get(dom_name)
+            # the counter passes were taken at the config's per-GPU size; another row count (strong
+            # scaling) has no entry: traffic stays null rather than another size's bytes
+            key = args.config if N == cfg["rows"] else f"{args.config}@{N}"
+            ent = tj.get(key, {}).get(dom_name)
             if ent:
                 traffic = ent.get("hbm_bytes_per_launch")
                 traffic_src = (f"read from {os.path.relpath(args.traffic, HERE)} (rocprofv3 FETCH_SIZE/WRITE_SIZE "

@@ -391,16 +391,17 @@ __global__ __launch_bounds__(M3_T) void k_mttkrp3_part(FactorSet fs, Mttkrp3Geom
   if (stop != nullptr && *stop != 0) return;
   __shared__ __attribute__((aligned(16))) float sG[M3_TILE];
   __shared__ float sQ[M3_FQR];    // Phi_q [k][r]
-  __shared__ float sM[64 * 16];   // Phi_m rows of the block [j][r] times Phi_s[i, r]
+  __shared__ float sM[64 * 16];   // Phi_m rows of the block [j][r]
   __shared__ float sH[64 * 16];   // H[j][r]
-  __shared__ float sS[16];
   const int t = threadIdx.x, R = g.R, Iq = g.Iq;
   const int i = blockIdx.x / g.NJ, jb = blockIdx.x - i * g.NJ;
   const int j0 = jb * g.JB, nj = g.Im - j0 < g.JB ? g.Im - j0 : g.JB;
   const float* __restrict__ Ps = phi + fs.off[g.fs_];
   const float* __restrict__ Pm = phi + fs.off[g.fm];
   const float* __restrict__ Pq = phi + fs.off[g.fq];
-  // the block's G rows: nj * Iq contiguous floats
+  // every global read of the workgroup at once: the block's G rows (nj * Iq contiguous floats),
+  // Phi_q, the block's Phi_m rows; this thread's Phi_s[i][r] (the rank r of its outputs below is
+  // t % R for every e = t + 256 c when R divides 256, else re-read per output)
   const float* __restrict__ Gb = G + ((int64_t)i * g.Im + j0) * Iq;
   const int ng = nj * Iq;
   if ((((uintptr_t)Gb) & 15) == 0 && (ng & 3) == 0) {
@@ -410,85 +411,95 @@ __global__ __launch_bounds__(M3_T) void k_mttkrp3_part(FactorSet fs, Mttkrp3Geom
     for (int e = t; e < ng; e += M3_T) sG[e] = Gb[e];
   }
   for (int e = t; e < Iq * R; e += M3_T) sQ[e] = Pq[e];
-  if (t < R) sS[t] = Ps[(int64_t)i * R + t];
+  for (int e = t; e < nj * R; e += M3_T) sM[e] = Pm[(int64_t)j0 * R + e];
   __syncthreads();
-  for (int e = t; e < nj * R; e += M3_T) {
-    const int r = e % R;
-    sM[e] = Pm[(int64_t)(j0 + e / R) * R + r] * sS[r];
-  }
-  // H[j][r] = sum_k G[j][k] Phi_q[k][r]   (nj x R outputs)
+  float* slab = part + (int64_t)blockIdx.x * g.slab;
+  // slab: [ s-partial (R) | m-partials (JB x R) | q-partials (Iq x R) ]
+  // H[j][r] = sum_k G[j][k] Phi_q[k][r] (nj x R); its m partial H Phi_s[i, r]
   for (int e = t; e < nj * R; e += M3_T) {
     const int j = e / R, r = e - j * R;
     const float* gr = sG + j * Iq;
     float h = 0.f;
     for (int k = 0; k < Iq; ++k) h = fmaf(gr[k], sQ[k * R + r], h);
     sH[e] = h;
+    slab[R + e] = h * Ps[(int64_t)i * R + r];
   }
-  __syncthreads();
-  float* slab = part + (int64_t)blockIdx.x * g.slab;
-  // slab: [ s-partial (R) | m-partials (JB x R) | q-partials (Iq x R) ]
-  if (t < R) {  // sum_j H[j][r] Phi_m[j][r] (times Phi_s only in the m partial)
-    float a = 0.f;
-    for (int j = 0; j < nj; ++j) a = fmaf(sH[j * R + t], Pm[(int64_t)(j0 + j) * R + t], a);
-    slab[t] = a;
-  }
-  for (int e = t; e < nj * R; e += M3_T) slab[R + e] = sH[e] * sS[e % R];
   // q partial[k][r] = sum_j G[j][k] Phi_m[j][r] Phi_s[i][r]
   for (int e = t; e < Iq * R; e += M3_T) {
     const int k = e / R, r = e - k * R;
     float a = 0.f;
     for (int j = 0; j < nj; ++j) a = fmaf(sG[j * Iq + k], sM[j * R + r], a);
-    slab[R + g.JB * R + e] = a;
+    slab[R + g.JB * R + e] = a * Ps[(int64_t)i * R + r];
+  }
+  __syncthreads();
+  if (t < R) {  // s partial: sum_j H[j][r] Phi_m[j][r]
+    float a = 0.f;
+    for (int j = 0; j < nj; ++j) a = fmaf(sH[j * R + t], sM[j * R + t], a);
+    slab[t] = a;
   }
 }
 
-// sum of n values at a stride in a fixed order: eight interleaved running sums, combined by a
-// fixed tree (a single running sum over the 128 block partials of config 4 doubled the fast
-// factor's distance from fp64 against k_mttkrp's per-row butterfly)
-__device__ __forceinline__ float m3_sum(const float* __restrict__ p, int64_t stride, int n) {
-  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  int b = 0;
-  for (; b + 8 <= n; b += 8) {
+// sum of the values b = q, q + 4, q + 8, ... (< n) at a stride: four interleaved running sums,
+// all loads of a trip in flight together
+__device__ __forceinline__ float m3_sum_q(const float* __restrict__ p, int64_t stride, int n, int q) {
+  float a[4] = {0.f, 0.f, 0.f, 0.f};
+  int b = q;
+  for (; b + 12 < n; b += 16) {
+    float v[4];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) a[u] += p[(int64_t)(b + u) * stride];
+    for (int u = 0; u < 4; ++u) v[u] = p[(int64_t)(b + 4 * u) * stride];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) a[u] += v[u];
   }
-  for (int u = 0; b + u < n; ++u) a[u] += p[(int64_t)(b + u) * stride];
-  return ((a[0] + a[4]) + (a[2] + a[6])) + ((a[1] + a[5]) + (a[3] + a[7]));
+  for (int u = 0; b < n; b += 4, ++u) a[u & 3] += p[(int64_t)b * stride];
+  return (a[0] + a[2]) + (a[1] + a[3]);
 }
 
+// 64 outputs per workgroup, each summed by four waves (wave q: partials q, q + 4, ...) and the four
+// quarter sums added in a fixed order (a single running sum over config 4's 128 block partials
+// doubled the fast factor's distance from fp64 against k_mttkrp's per-row butterfly; one thread
+// per output left 16 dependent L2 round trips on the critical path)
 __global__ __launch_bounds__(M3_T) void k_mttkrp3_sum(FactorSet fs, Mttkrp3Geom g, const float* __restrict__ dphi,
                                                       const float* __restrict__ w, const float* __restrict__ part,
                                                       float* __restrict__ out, const int32_t* __restrict__ stop) {
   if (stop != nullptr && *stop != 0) return;
+  __shared__ float red[4][64];
   const int R = g.R;
-  const int64_t e = (int64_t)blockIdx.x * M3_T + threadIdx.x;
+  const int ol = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int64_t e = (int64_t)blockIdx.x * 64 + ol;
   const int64_t ns = (int64_t)g.Is * R, nm = (int64_t)g.Im * R, nq = (int64_t)g.Iq * R;
-  if (e >= ns + nm + nq) return;
+  const bool ok = e < ns + nm + nq;
   float acc = 0.f;
-  int f;
-  int64_t row;
-  int r;
-  if (e < ns) {  // dA_s[i][r]: the NJ blocks of row i
+  int f = 0;
+  int64_t row = 0;
+  int r = 0;
+  if (!ok) {
+  } else if (e < ns) {  // dA_s[i][r]: the NJ blocks of row i
     f = g.fs_;
     row = e / R;
     r = (int)(e - row * R);
-    acc = m3_sum(part + row * g.NJ * g.slab + r, g.slab, g.NJ);
+    acc = m3_sum_q(part + row * g.NJ * g.slab + r, g.slab, g.NJ, q);
   } else if (e < ns + nm) {  // dA_m[j][r]: every i of j's block
     f = g.fm;
     const int64_t x = e - ns;
     row = x / R;
     r = (int)(x - row * R);
     const int jb = (int)(row / g.JB), jj = (int)(row - (int64_t)jb * g.JB);
-    acc = m3_sum(part + (int64_t)jb * g.slab + R + jj * R + r, (int64_t)g.NJ * g.slab, g.Is);
+    acc = m3_sum_q(part + (int64_t)jb * g.slab + R + jj * R + r, (int64_t)g.NJ * g.slab, g.Is, q);
   } else {  // dA_q[k][r]: every block
     f = g.fq;
     const int64_t x = e - ns - nm;
     row = x / R;
     r = (int)(x - row * R);
-    acc = m3_sum(part + R + (int64_t)g.JB * R + x, g.slab, g.Is * g.NJ);
+    acc = m3_sum_q(part + R + (int64_t)g.JB * R + x, g.slab, g.Is * g.NJ, q);
   }
-  const int64_t o = fs.off[f] + row * R + r;
-  out[o] = acc * w[r] * dphi[o];
+  red[q][ol] = acc;
+  __syncthreads();
+  if (q == 0 && ok) {
+    const float s = (red[0][ol] + red[1][ol]) + (red[2][ol] + red[3][ol]);
+    const int64_t o = fs.off[f] + row * R + r;
+    out[o] = s * w[r] * dphi[o];
+  }
 }
 
 bool mttkrp3_supported(const FactorSet& fs, int64_t part_cap) {
@@ -503,8 +514,8 @@ hipError_t launch_mttkrp3(const FactorSet& fs, const float* phi, const float* dp
   if (!mttkrp3_geom(fs, &g) || (int64_t)g.Is * g.NJ * g.slab > part_cap) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_mttkrp3_part, dim3((unsigned)(g.Is * g.NJ)), dim3(M3_T), 0, st, fs, g, phi, G, part, stop);
   const int64_t nout = (int64_t)(g.Is + g.Im + g.Iq) * g.R;
-  hipLaunchKernelGGL(k_mttkrp3_sum, dim3((unsigned)((nout + M3_T - 1) / M3_T)), dim3(M3_T), 0, st, fs, g, dphi, w,
-                     part, grad, stop);
+  hipLaunchKernelGGL(k_mttkrp3_sum, dim3((unsigned)((nout + 63) / 64)), dim3(M3_T), 0, st, fs, g, dphi, w, part,
+                     grad, stop);
   return hipGetLastError();
 }
 
