@@ -41,13 +41,20 @@ struct MnlGeom {
   // one (i, j) block; LDS carve of ONE workgroup (floats)
   int duo;
   int du_oZ, du_oP1, du_oG, du_oPF, du_lds_floats;
-  // bf16-split form of the two-workgroups-per-CU kernel (k_mnl_bsp, the default where it fits:
-  // a 32 KiB (128, 64) or (64, 128) sample, R <= 8, C <= 16; TR_DUO_SPLIT=0 keeps the rank-block
-  // form): U partials at bs_oU
+  // bf16-split form of the duo family (k_mnl_bsp: a 32 KiB (128, 64) or (64, 128) sample at
+  // rank <= 4, and every (32 NW, 64) sample with NW = 2..8 at rank <= 8, C <= 16; TR_DUO_SPLIT=1
+  // takes it at (128, 64) / (64, 128) rank 5..8 too, =0 keeps the rank-block form): U partials at bs_oU
   int bsp, bs_oU;
+  // waves per workgroup and workgroups per CU of the two-workgroups-per-CU family (4, 2; the
+  // split body on (32 NW, 64) samples: NW, 8 / NW)
+  int du_nw, du_wpc;
+  // k_mnl_fused fits this shape (mnl_geom_init may accept a shape only the split body runs)
+  int fused_ok;
 };
 
-// Fills g; false (with a reason) when the shape is outside the kernel's envelope.
+// Fills g; false (with a reason) when the shape is outside the factored kernels' envelope.  A
+// shape k_mnl_fused does not fit (more than 8 GEMM units, its LDS ring) returns true with
+// g->fused_ok = 0 (and the reason): only the split body of tr_mnl_duo.hip can run it.
 bool mnl_geom_init(MnlGeom* g, int64_t I, int64_t J, int R, int C, std::string* why);
 // Sets the dynamic-LDS limit and checks the instantiation is spill-free and fits a CU.
 hipError_t mnl_prepare(const MnlGeom& g, int* ok);
@@ -63,7 +70,7 @@ hipError_t launch_mnl_fused(const MnlGeom& g, int grid, const float* X, int64_t 
 // kernel is spill-free and two of its workgroups fit a CU.
 void mnl_duo_geom(MnlGeom* g);
 hipError_t mnl_duo_prepare(MnlGeom* g);
-// Same contract as launch_mnl_fused, with grid = 2 workgroups per CU.
+// Same contract as launch_mnl_fused, with grid = g.du_wpc workgroups per CU.
 hipError_t launch_mnl_duo(const MnlGeom& g, int grid, const float* X, int64_t N, int64_t xld, const float* phi,
                           const float* w, const int64_t* lab, const float* class_w, float scale, float* gpart,
                           double* dpart, int64_t rows_per_wg, int reverse, const int32_t* stop, hipStream_t st);

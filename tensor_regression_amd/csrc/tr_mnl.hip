@@ -675,7 +675,12 @@ bool mnl_geom_init(MnlGeom* g, int64_t I, int64_t J, int R, int C, std::string* 
   g->Rp = 4 * g->nrb;
   g->nA = g->nib * g->njb * g->nrb;
   g->nunits = 2 * g->nA;
-  if (g->nunits > MN_NW) return no("more than 8 GEMM units (I, J or R too large)");
+  g->fused_ok = 1;
+  auto no_fused = [&](const char* m) {
+    if (why) *why = m;
+    g->fused_ok = 0;
+  };
+  if (g->nunits > MN_NW) no_fused("more than 8 GEMM units (I, J or R too large)");
   g->upw = 1;
   g->nsets = g->nib * g->njb;
   g->full = (I % 64 == 0 && J % 64 == 0) ? 1 : 0;
@@ -705,13 +710,14 @@ bool mnl_geom_init(MnlGeom* g, int64_t I, int64_t J, int R, int C, std::string* 
     o += g->slab;
   }
   o = (o + 3) & ~(int64_t)3;
-  if (o * 4 > 160 * 1024) return no("LDS budget exceeded");
-  g->lds_floats = (int)o;
+  if (o * 4 > 160 * 1024) no_fused("LDS budget exceeded");
+  g->lds_floats = g->fused_ok ? (int)o : 0;
   return true;
 }
 
 hipError_t mnl_prepare(const MnlGeom& g, int* ok) {
   *ok = 0;
+  if (!g.fused_ok) return hipSuccess;
   const void* k = mnl_kernel(g);
   const size_t lds = (size_t)g.lds_floats * 4;
   hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -603,27 +603,30 @@ __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, cons
 // that one 16-wide MFMA carries every piece product of weight >= 2^-17:
 //   B12 = [b1 | b2] (columns 0-7 | 8-15, rank = column & 7), B3 = [b3 | 0]
 //   acc += x1.B12 + x2.B12 + x1.B3  ->  column r + column r + 8 = x1b1 + x1b2 + x2b1 + x2b2 + x1b3
-// A sample (I x J = 8192 floats) takes 96 MFMAs per workgroup instead of 512 4x4x1 ones: the
-// rank-block form spends 1,024 issue cycles per wave-sample on MFMAs alone.  Work of wave wv:
+// A 32 KiB sample takes 96 MFMAs per workgroup instead of 512 4x4x1 ones: the rank-block form
+// spends 1,024 issue cycles per wave-sample on MFMAs alone.  J = 64 samples of 32 NW rows run NW
+// waves (NW = 2..8, 8 / NW workgroups per CU), J = 128 ones (64 rows) four.  Work of wave wv:
 //   T[i, r] over i-tiles of 16 rows (J = 64: tiles 2 wv, 2 wv + 1; J = 128: tile wv) and every
 //     32-deep j k-step: A = X rows (two ds_read_b128 of consecutive chunks per lane)
 //   V[j, r] over 4 j-tiles for ONE 32-deep i k-step (J = 64: k-step wv; J = 128: k-step wv & 1,
 //     chunk group wv >> 1): j-tile t holds j = 4 c + t for chunk c = lane row, so one ds_read_b128
 //     of chunk c of row i gives element i of four tiles (eight reads: the k-step's 32 i)
 // The chunk swizzle q ^ (i & 15) makes both reads conflict-free.  T is complete per wave (its
-// U partial over its rows goes through LDS: four partials per sample); V is a partial over the
+// U partial over its rows goes through LDS: NW partials per sample); V is a partial over the
 // wave's i k-step, and dPhi1 = sum_n Wv_n V_n is linear in it: the waves' partials are summed
 // once, at the end.  Every wave runs the softmax epilogue of the previous sample (staged between
 // its GEMM steps) for all 8 ranks; wave 0 alone accumulates dPhiC and the loss.
-template <int JT>
+template <int JT, int NW>
 __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, const int64_t* __restrict__ lab,
                                          const float* __restrict__ class_w, float* lds, const int wv, const int lane) {
   const int t = threadIdx.x;
-  constexpr int J = JT, I = 8192 / JT, SPF = 8192, JQ = J / 4;
-  constexpr int NT = I / 64;   // T i-tiles per wave
+  // J = 64: NW waves, each owning 32 rows of an (32 NW, 64) sample; J = 128: (64, 128), four waves
+  constexpr int J = JT, I = JT == 64 ? 32 * NW : 8192 / JT, SPF = I * J, JQ = J / 4, NT_ = NW * TR_WAVE;
+  static_assert(JT == 64 || NW == 4, "the (64, 128) body runs four waves");
+  constexpr int NT = JT == 64 ? 2 : I / 64;  // T i-tiles per wave
   constexpr int NKT = J / 32;  // T k-steps (j)
   const int R = g.R, C = g.C;
-  float* sU = lds + g.bs_oU;  // [2 parity][4 waves][8 ranks] U partials
+  float* sU = lds + g.bs_oU;  // [2 parity][NW waves][8 ranks] U partials
   const float* P0 = a.phi;
   const float* P1 = a.phi + g.offP1;
   const float* PC = a.phi + g.offPC;
@@ -641,7 +644,7 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
   for (int r = 0; r < 8; ++r) rsel[r] = r8 == r ? 1.f : 0.f;
 
   const int it0 = NT == 2 ? 32 * wv : 16 * wv;                    // first T row of this wave
-  const int iv0 = I == 128 ? 32 * wv : 32 * (wv & 1);             // V k-step (rows) of this wave
+  const int iv0 = JT == 64 ? 32 * wv : 32 * (wv & 1);             // V k-step (rows) of this wave
   const int cv = n + (J == 128 ? 16 * (wv >> 1) : 0);             // V chunk (j = 4 cv + tile)
   // B operands, split once per launch: T (Phi1, element e of lane group gq <-> j = 32 s + 8 gq + e)
   uint32_t bT12[NKT][4], bT3[NKT][4], hT[NKT][4], bV12[4], bV3[4], hV[4];
@@ -683,13 +686,13 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
   for (int r = 0; r < 8; ++r) pc[r] = (cok && r < R) ? a.w[r] * PC[c * R + r] : 0.f;
   const float pcg0 = pc[gq & 3], pcg1 = pc[4 + (gq & 3)];
   const float wg0 = gq < R ? a.w[gq] : 0.f, wg1 = gq + 4 < R ? a.w[gq + 4] : 0.f;
-  for (int e = t; e < 2 * 4 * 8; e += DU_T) sU[e] = 0.f;
+  for (int e = t; e < 2 * NW * 8; e += NT_) sU[e] = 0.f;
 
-  // LDS-DMA map (as the rank-block form): wave wv issues the 1 KiB groups wv + 4 gi of every sample
+  // LDS-DMA map (as the rank-block form): wave wv issues the 1 KiB groups wv + NW gi of every sample
   uint32_t goff[8];
 #pragma unroll
   for (int gi = 0; gi < 8; ++gi) {
-    const int slot = (wv + DU_NW * gi) * TR_WAVE + lane;
+    const int slot = (wv + NW * gi) * TR_WAVE + lane;
     const int i = slot / JQ;
     const int q = slot - i * JQ;
     goff[gi] = 4u * (uint32_t)(i * J + 4 * (q ^ (i & 15)));
@@ -742,9 +745,11 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
   bool e_isy = false;
   auto epi = [&](int st, int zs, int64_t yE, float cwE) {
     if (TR_DUO_SKIP & 4) return;
-    if (st == 0) {  // U[r] = sum of the four waves' partials (lane r), wave order
-      const float* pu = sU + zs * 32 + r8;
-      uS = ((pu[0] + pu[8]) + pu[16]) + pu[24];
+    if (st == 0) {  // U[r] = sum of the NW waves' partials (lane r), wave order
+      const float* pu = sU + zs * (8 * NW) + r8;
+      uS = pu[0];
+#pragma unroll
+      for (int w = 1; w < NW; ++w) uS += pu[8 * w];
     } else if (st == 1) {
 #pragma unroll
       for (int r = 0; r < 8; ++r) uR[r] = du_rdl(uS, r);
@@ -807,7 +812,7 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
   auto dma_sample = [&](const float* src, int slot) {
 #pragma unroll
     for (int gi = 0; gi < 8; ++gi)
-      du_dma_s(goff[gi], src, lbase + (uint32_t)(slot * 4 * SPF) + (uint32_t)(wv + DU_NW * gi) * 1024u);
+      du_dma_s(goff[gi], src, lbase + (uint32_t)(slot * 4 * SPF) + (uint32_t)(wv + NW * gi) * 1024u);
   };
   // two samples in flight per workgroup: sample k + 2 goes into slot k & 1 as soon as every wave
   // holds its operands of k in registers (a second barrier per sample); the kernel is bound by the
@@ -859,7 +864,7 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
     if (TIF) du_barrier();  // (its lgkmcnt(0): this wave's reads landed) every wave's operands of k read
 #pragma unroll
     for (int st = 0; st < NU + 4; ++st) {
-      if (!(TR_DUO_SKIP & 8)) du_dma_s(goff[st], psrc, pm0 + (uint32_t)st * 4096u);
+      if (!(TR_DUO_SKIP & 8)) du_dma_s(goff[st], psrc, pm0 + (uint32_t)st * (uint32_t)(NW * 1024));
       sl_u4 x1, x2;
       if (st < NU) {
 #pragma unroll
@@ -909,7 +914,7 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
       VP[q] = aV[q];
     }
     u = du_xor32_sum(du_xor16_sum(u));  // lane (n < 8, any row): this wave's U partial of rank n
-    if (lane < 8) sU[SL * 32 + wv * 8 + lane] = u;
+    if (lane < 8) sU[SL * (8 * NW) + wv * 8 + lane] = u;
     yP = yC;
     cwP = cwC;
     TR_DUO_MARK(3);
@@ -932,9 +937,9 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
   // ---- fixed-order reduction into an LDS image of the arena (wave order), slab ----
   float* sG = lds + g.du_oG;
   __syncthreads();
-  for (int64_t e = t; e < g.slab; e += DU_T) sG[e] = 0.f;
+  for (int64_t e = t; e < g.slab; e += NT_) sG[e] = 0.f;
   __syncthreads();
-  for (int ws = 0; ws < DU_NW; ++ws) {
+  for (int ws = 0; ws < NW; ++ws) {
     if (ws == wv && lo8 && rok) {
 #pragma unroll
       for (int tt = 0; tt < NT; ++tt)
@@ -962,17 +967,20 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
     }
   }
   float* slab = a.gpart + (int64_t)blockIdx.x * g.slab;
-  for (int64_t e = t; e < g.slab; e += DU_T) slab[e] = sG[e];
+  for (int64_t e = t; e < g.slab; e += NT_) slab[e] = sG[e];
 }
 
-template <int JT>
-__global__ __launch_bounds__(DU_T, 2) void k_mnl_bsp(MnlGeom g, DuArgs a, const int64_t* __restrict__ lab,
-                                                  const float* __restrict__ class_w, const int32_t* __restrict__ stop) {
+// NW waves per workgroup, 8 / NW workgroups per CU (the second bound is waves per SIMD: two,
+// 256 VGPRs each)
+template <int JT, int NW>
+__global__ __launch_bounds__(NW * TR_WAVE, 2) void k_mnl_bsp(MnlGeom g, DuArgs a, const int64_t* __restrict__ lab,
+                                                               const float* __restrict__ class_w,
+                                                               const int32_t* __restrict__ stop) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   if (stop != nullptr && *stop != 0) return;
   const int lane = threadIdx.x & (TR_WAVE - 1);
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / TR_WAVE);
-  bsp_body<JT>(g, a, lab, class_w, lds, wv, lane);
+  bsp_body<JT, NW>(g, a, lab, class_w, lds, wv, lane);
 }
 
 template <int JT>
@@ -988,30 +996,54 @@ __global__ __launch_bounds__(DU_T, 2) void k_mnl_duo(MnlGeom g, DuArgs a, const 
 // ------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------
+// the split body's instantiations: (32 NW, 64) samples with NW = 2..8 waves, (64, 128) with four
+template <int JT, int NW>
+static const void* bsp_ptr() {
+  return reinterpret_cast<const void*>(&k_mnl_bsp<JT, NW>);
+}
 static const void* duo_kernel(const MnlGeom& g) {
-  if (g.bsp)
-    return g.J == 64 ? reinterpret_cast<const void*>(&k_mnl_bsp<64>) : reinterpret_cast<const void*>(&k_mnl_bsp<128>);
+  if (g.bsp) {
+    if (g.J == 128) return bsp_ptr<128, 4>();
+    switch (g.du_nw) {
+      case 2: return bsp_ptr<64, 2>();
+      case 3: return bsp_ptr<64, 3>();
+      case 4: return bsp_ptr<64, 4>();
+      case 5: return bsp_ptr<64, 5>();
+      case 6: return bsp_ptr<64, 6>();
+      case 7: return bsp_ptr<64, 7>();
+      case 8: return bsp_ptr<64, 8>();
+      default: return nullptr;
+    }
+  }
   return g.J == 64 ? reinterpret_cast<const void*>(&k_mnl_duo<64>) : reinterpret_cast<const void*>(&k_mnl_duo<128>);
 }
 
 void mnl_duo_geom(MnlGeom* g) {
   g->duo = 0;
   g->bsp = 0;
+  g->du_nw = 4;
+  g->du_wpc = 2;
   const char* env = std::getenv("TR_MNL_DUO");
   if (env != nullptr && env[0] == '0') return;
-  // compiled shapes: a 32 KiB sample as (128, 64) or (64, 128) (two 64-row blocks, 8 LDS-DMA
-  // groups per wave, chunk swizzle q ^ (i & 15))
-  if (!g->full || g->I * g->J != 8192 || (g->J != 64 && g->J != 128) || g->C > kMnlCMax) return;
-  if (g->smask != 15) return;
+  if (g->C > kMnlCMax || g->smask != 15 || (g->J != 64 && g->J != 128)) return;
+  // compiled shapes: the rank-block body takes a 32 KiB sample as (128, 64) or (64, 128) (two
+  // 64-row blocks, 8 LDS-DMA groups per wave, chunk swizzle q ^ (i & 15)); the split body takes
+  // those and every (32 NW, 64) sample, NW = 2..8 (one wave per 32 rows, 8 / NW workgroups per CU)
+  const bool s32k = g->full && g->I * g->J == 8192;
+  const bool wide = g->J == 64 && g->I % 32 == 0 && g->I / 32 >= 2 && g->I / 32 <= 8;
   // form: the f32 rank-block body where it fits (R in 5..8: two rank blocks), the bf16-split body
-  // for R <= 4; TR_DUO_SPLIT=1 takes the split body for R <= 8, =0 the rank-block body only.
-  // (With the non-temporal sample DMA both run at the same rate at c3 — 0.339 / 0.343-0.347 ms,
-  // the sample stream bounds them — and the rank-block form is the more accurate: 3.1e-7 vs
-  // 7.2e-7 normwise from fp64 at full c3 size, the reference's own fp32 7.8e-7.)
+  // for R <= 4 and for the other (I, 64) shapes; TR_DUO_SPLIT=1 takes the split body for R <= 8,
+  // =0 the rank-block body only.  (With the non-temporal sample DMA both run at the same rate at
+  // c3 — 0.339 / 0.343-0.347 ms, the sample stream bounds them — and the rank-block form is the
+  // more accurate: 3.1e-7 vs 7.2e-7 normwise from fp64 at full c3 size; the reference's own op
+  // sequence in fp32 at the same factors 4.0e-6.)
   const char* spl = std::getenv("TR_DUO_SPLIT");
   const bool force_split = spl != nullptr && spl[0] == '1', no_split = spl != nullptr && spl[0] == '0';
-  const bool bsp = g->R <= 8 && !no_split && (force_split || g->nrb != 2);
-  if (!bsp && g->nrb != 2) return;
+  const bool rankblock = s32k && g->nrb == 2;
+  const bool bsp = (s32k || wide) && g->R <= 8 && !no_split && (force_split || !rankblock);
+  if (!bsp && !rankblock) return;
+  const int nw = bsp && g->J == 64 ? g->I / 32 : 4;
+  const int wpc = 8 / nw;
   const int64_t spf = (int64_t)g->I * g->J;
   int64_t o = 2 * spf;  // ring of two samples
   g->du_oZ = (int)o;
@@ -1021,19 +1053,25 @@ void mnl_duo_geom(MnlGeom* g) {
   o = (o + 3) & ~(int64_t)3;
   g->du_oPF = (int)o;  // prefetch scratch line (64 dwords, written by every wave, never read)
   o += TR_WAVE;
-  g->bs_oU = (int)o;  // bsp: [2][4 waves][8 ranks] U partials
-  o += 2 * 4 * 8;
+  g->bs_oU = (int)o;  // bsp: [2][NW waves][8 ranks] U partials
+  o += 2 * nw * 8;
   g->du_oG = g->slab <= 2 * spf ? 0 : (int)o;  // the arena image aliases the drained ring
   if (g->du_oG) o += g->slab;
   o = (o + 3) & ~(int64_t)3;
-  if (2 * o * 4 > 160 * 1024) return;  // two workgroups per CU
+  if (wpc * o * 4 > 160 * 1024) return;  // wpc workgroups per CU
   g->du_lds_floats = (int)o;
+  g->du_nw = nw;
+  g->du_wpc = wpc;
   g->duo = 1;
   g->bsp = bsp ? 1 : 0;
 }
 
 static hipError_t duo_kernel_ok(const MnlGeom& g, bool* ok) {
   const void* k = duo_kernel(g);
+  if (k == nullptr) {
+    *ok = false;
+    return hipSuccess;
+  }
   const size_t lds = (size_t)g.du_lds_floats * 4;
   hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
@@ -1041,9 +1079,9 @@ static hipError_t duo_kernel_ok(const MnlGeom& g, bool* ok) {
   e = hipFuncGetAttributes(&attr, k);
   if (e != hipSuccess) return e;
   int nb = 0;
-  e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, DU_T, lds);
+  e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, g.du_nw * TR_WAVE, lds);
   if (e != hipSuccess) return e;
-  *ok = attr.localSizeBytes == 0 && nb >= 2;  // no spills, two per CU
+  *ok = attr.localSizeBytes == 0 && nb >= g.du_wpc;  // no spills, du_wpc per CU
   return hipSuccess;
 }
 
@@ -1053,14 +1091,18 @@ hipError_t mnl_duo_prepare(MnlGeom* g) {
   hipError_t e = duo_kernel_ok(*g, &ok);
   if (e != hipSuccess) return e;
   if (ok) return hipSuccess;
-  if (g->bsp && g->nrb == 2) {  // the rank-block form instead
+  if (g->bsp && g->full && g->I * g->J == 8192 && g->nrb == 2) {  // the rank-block form instead
     g->bsp = 0;
+    g->du_nw = 4;
+    g->du_wpc = 2;
     e = duo_kernel_ok(*g, &ok);
     if (e != hipSuccess) return e;
     if (ok) return hipSuccess;
   }
-  g->duo = 0;  // k_mnl_fused
+  g->duo = 0;  // k_mnl_fused (where it fits)
   g->bsp = 0;
+  g->du_nw = 4;
+  g->du_wpc = 2;
   return hipSuccess;
 }
 
@@ -1071,10 +1113,23 @@ hipError_t launch_mnl_duo(const MnlGeom& g, int grid, const float* X, int64_t N,
   DuArgs a{X, N, xld, phi, w, scale, gpart, dpart, rows_per_wg, reverse};
   const size_t lds = (size_t)g.du_lds_floats * 4;
   if (g.bsp) {
-    if (g.J == 64)
-      hipLaunchKernelGGL((k_mnl_bsp<64>), dim3(grid), dim3(DU_T), lds, st, g, a, lab, class_w, stop);
-    else
-      hipLaunchKernelGGL((k_mnl_bsp<128>), dim3(grid), dim3(DU_T), lds, st, g, a, lab, class_w, stop);
+#define TR_BSP_LAUNCH(JT, NW) \
+  hipLaunchKernelGGL((k_mnl_bsp<JT, NW>), dim3(grid), dim3(NW * TR_WAVE), lds, st, g, a, lab, class_w, stop)
+    if (g.J == 128) {
+      TR_BSP_LAUNCH(128, 4);
+    } else {
+      switch (g.du_nw) {
+        case 2: TR_BSP_LAUNCH(64, 2); break;
+        case 3: TR_BSP_LAUNCH(64, 3); break;
+        case 4: TR_BSP_LAUNCH(64, 4); break;
+        case 5: TR_BSP_LAUNCH(64, 5); break;
+        case 6: TR_BSP_LAUNCH(64, 6); break;
+        case 7: TR_BSP_LAUNCH(64, 7); break;
+        case 8: TR_BSP_LAUNCH(64, 8); break;
+        default: return hipErrorInvalidValue;
+      }
+    }
+#undef TR_BSP_LAUNCH
   } else if (g.J == 64) {
     hipLaunchKernelGGL((k_mnl_duo<64>), dim3(grid), dim3(DU_T), lds, st, g, a, lab, class_w, stop);
   } else {

@@ -367,6 +367,10 @@ def test_linear_sweep_vs_oracle(shape, rank, kind):
                                    atol=RTOL * np.abs(ref["y_hat"]).max())
 
 
+# (shape, C, rank) of the split body's (32 NW, 64) sample shapes: one per wave count, a rank-8
+# model on two rank blocks, fewer samples than workgroups, one rank
+WIDE_SHAPES = [((300, 64, 64), 10, 8), ((200, 96, 64), 7, 3), ((400, 128, 64), 5, 2), ((90, 160, 64), 4, 8),
+               ((33, 192, 64), 12, 4), ((60, 224, 64), 3, 6), ((150, 256, 64), 16, 5), ((5, 64, 64), 2, 1)]
 MNL_SHAPES = [((50, 8, 4), 2, 2), ((200, 16, 8), 10, 4), ((97, 5, 7), 16, 3), ((64, 33), 3, 1),
               ((128, 4, 4, 4), 5, 6), ((333, 32, 32), 10, 8), ((40, 64), 16, 2), ((3, 32), 3, 2),
               # factored single pass: ragged 64-blocks, R % 4 != 0, k ranges split over 2 blocks,
@@ -376,6 +380,8 @@ MNL_SHAPES = [((50, 8, 4), 2, 2), ((200, 16, 8), 10, 4), ((97, 5, 7), 16, 3), ((
               # two-workgroups-per-CU variant: R % 4 != 0 over two rank blocks, one rank block,
               # fewer samples than workgroups, J = 128
               ((1001, 128, 64), 10, 5), ((513, 128, 64), 16, 3), ((2, 128, 64), 2, 8), ((300, 64, 128), 6, 7),
+              # its split body on (32 NW, 64) samples, NW = 2..8 (I = 256: k_mnl_fused does not fit)
+              *WIDE_SHAPES,
               # wide classes (C > 16): logits by class tile (MFMA when P % 32 == 0, else VALU),
               # k_softmax_rows, tiled column reduction; rank beyond 64 (MTTKRP rank tiles)
               ((150, 8, 4), 17, 3), ((230, 16, 8), 40, 5), ((99, 5, 7), 33, 2), ((200, 12), 100, 4),
@@ -387,6 +393,15 @@ MNL_SHAPES = [((50, 8, 4), 2, 2), ((200, 16, 8), 10, 4), ((97, 5, 7), 16, 3), ((
 def test_multinomial_sweep_vs_oracle(shape, C, rank, kind):
     with path(kind):
         _multinomial_sweep(shape, C, rank)
+
+
+@pytest.mark.parametrize("shape,C,rank", WIDE_SHAPES)
+def test_multinomial_wide_split_body_selected(shape, C, rank):
+    """(32 NW, 64) samples with R <= 8 take the split body with NW waves per workgroup by default
+    (describe 'form=bf16split waves=NW'); the results are the sweep's."""
+    with path("auto"):
+        desc = _multinomial_sweep(shape, C, rank)
+    assert "form=bf16split" in desc and f"waves={shape[1] // 32} wg/cu={8 // (shape[1] // 32)} " in desc, desc
 
 
 def _multinomial_sweep(shape, C, rank):
@@ -419,6 +434,7 @@ def _multinomial_sweep(shape, C, rank):
     _assert_factors(plan.factor_views(gtot), ref["grads"])
     S = plan.forward(Xd, arena, mm.weights)
     np.testing.assert_allclose(S.cpu().numpy(), ref["probs"], rtol=RTOL, atol=1e-6)
+    return plan.describe
 
 
 @pytest.mark.parametrize("shape", [(3000, 64, 32), (700, 64, 64, 32)])

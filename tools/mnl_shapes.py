@@ -5,7 +5,7 @@
 
 For each (I, J) the sample count N fills ~2 GiB of X; fit_Adam runs 200 warm-up iterations, then
 30 with the stream kernel timed by hipEvents.  Prints the plan's path (k_mnl_duo in its rank-block
-or bf16-split form, or k_mnl_fused, or the two-pass kernels) and the stream kernel's rate against
+or bf16-split form and its wave count, or k_mnl_fused, or the two-pass kernels) and the stream kernel's rate against
 its algorithmic bytes (4 I J + 8 per sample) and the 8 TB/s HBM peak.
 """
 import os
@@ -18,8 +18,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from tensor_regression_amd import CP_logistic_regression  # noqa: E402
 
 dev = "cuda:0"
-SHAPES = [((128, 64), 8), ((64, 128), 8), ((128, 64), 3), ((64, 64), 8), ((256, 64), 8), ((128, 128), 8),
-          ((96, 64), 8), ((256, 128), 8)]
+SHAPES = [((128, 64), 8), ((64, 128), 8), ((128, 64), 3), ((64, 64), 8), ((96, 64), 8), ((160, 64), 8),
+          ((192, 64), 8), ((256, 64), 8), ((64, 64), 3), ((128, 128), 8), ((256, 128), 8)]
 C = 10
 for (I, J), R in SHAPES:
     N = (1 << 29) // (I * J)
@@ -41,7 +41,8 @@ for (I, J), R in SHAPES:
     tot = sum(ms.values())
     alg = N * (4 * I * J + 8)
     path = plan.describe.split(" path=")[1].split()[0]
-    form = ("duo " + plan.describe.split("form=")[1].split()[0]) if " duo " in plan.describe else path
+    form = (f"duo {plan.describe.split('form=')[1].split()[0]} waves={plan.describe.split('waves=')[1].split()[0]}"
+            if " duo " in plan.describe else path)
     print(f"(N, I, J) = ({N}, {I}, {J}) R={R}: {form:24s} stream kernels {tot:.4f} ms = "
           f"{alg / (tot * 1e-3) / 1e12:.2f} TB/s = {alg / (tot * 1e-3) / 8e12 * 100:.1f} % of HBM  {ms}", flush=True)
     del m, X, y
