@@ -605,11 +605,12 @@ __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, cons
 //   acc += x1.B12 + x2.B12 + x1.B3  ->  column r + column r + 8 = x1b1 + x1b2 + x2b1 + x2b2 + x1b3
 // A 32 KiB sample takes 96 MFMAs per workgroup instead of 512 4x4x1 ones: the rank-block form
 // spends 1,024 issue cycles per wave-sample on MFMAs alone.  J = 64 samples of 32 NW rows run NW
-// waves (NW = 2..8, 8 / NW workgroups per CU), J = 128 ones (64 rows) four.  Work of wave wv:
+// waves (NW = 2..8), J = 128 ones of 16 NW rows NW waves (NW = 4, 6, 8); 8 / NW workgroups per
+// CU.  Work of wave wv:
 //   T[i, r] over i-tiles of 16 rows (J = 64: tiles 2 wv, 2 wv + 1; J = 128: tile wv) and every
 //     32-deep j k-step: A = X rows (two ds_read_b128 of consecutive chunks per lane)
-//   V[j, r] over 4 j-tiles for ONE 32-deep i k-step (J = 64: k-step wv; J = 128: k-step wv & 1,
-//     chunk group wv >> 1): j-tile t holds j = 4 c + t for chunk c = lane row, so one ds_read_b128
+//   V[j, r] over 4 j-tiles for ONE 32-deep i k-step (J = 64: k-step wv; J = 128: k-step
+//     wv % (NW / 2), chunk group wv / (NW / 2)): j-tile t holds j = 4 c + t for chunk c = lane row, so one ds_read_b128
 //     of chunk c of row i gives element i of four tiles (eight reads: the k-step's 32 i)
 // The chunk swizzle q ^ (i & 15) makes both reads conflict-free.  T is complete per wave (its
 // U partial over its rows goes through LDS: NW partials per sample); V is a partial over the
@@ -620,10 +621,12 @@ template <int JT, int NW>
 __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, const int64_t* __restrict__ lab,
                                          const float* __restrict__ class_w, float* lds, const int wv, const int lane) {
   const int t = threadIdx.x;
-  // J = 64: NW waves, each owning 32 rows of an (32 NW, 64) sample; J = 128: (64, 128), four waves
-  constexpr int J = JT, I = JT == 64 ? 32 * NW : 8192 / JT, SPF = I * J, JQ = J / 4, NT_ = NW * TR_WAVE;
-  static_assert(JT == 64 || NW == 4, "the (64, 128) body runs four waves");
-  constexpr int NT = JT == 64 ? 2 : I / 64;  // T i-tiles per wave
+  // J = 64: NW waves, each owning 32 rows of a (32 NW, 64) sample; J = 128: NW waves over a
+  // (16 NW, 128) sample, each owning 16 T rows and one (32-row k-step, 16-chunk group) of V
+  constexpr int J = JT, I = JT == 64 ? 32 * NW : 16 * NW, SPF = I * J, JQ = J / 4, NT_ = NW * TR_WAVE;
+  static_assert(JT == 64 || NW % 2 == 0, "J = 128: two chunk groups per V k-step");
+  constexpr int NT = JT == 64 ? 2 : 1;  // T i-tiles per wave
+  constexpr int NKS = I / 32;           // V k-steps (J = 128: NW / 2 of them, two chunk groups each)
   constexpr int NKT = J / 32;  // T k-steps (j)
   const int R = g.R, C = g.C;
   float* sU = lds + g.bs_oU;  // [2 parity][NW waves][8 ranks] U partials
@@ -644,8 +647,8 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
   for (int r = 0; r < 8; ++r) rsel[r] = r8 == r ? 1.f : 0.f;
 
   const int it0 = NT == 2 ? 32 * wv : 16 * wv;                    // first T row of this wave
-  const int iv0 = JT == 64 ? 32 * wv : 32 * (wv & 1);             // V k-step (rows) of this wave
-  const int cv = n + (J == 128 ? 16 * (wv >> 1) : 0);             // V chunk (j = 4 cv + tile)
+  const int iv0 = JT == 64 ? 32 * wv : 32 * (wv % NKS);           // V k-step (rows) of this wave
+  const int cv = n + (J == 128 ? 16 * (wv / NKS) : 0);            // V chunk (j = 4 cv + tile)
   // B operands, split once per launch: T (Phi1, element e of lane group gq <-> j = 32 s + 8 gq + e)
   uint32_t bT12[NKT][4], bT3[NKT][4], hT[NKT][4], bV12[4], bV3[4], hV[4];
   auto bsplit = [&](float x0, float x1, uint32_t& b12, uint32_t& b3, uint32_t& hh) {
@@ -1003,7 +1006,14 @@ static const void* bsp_ptr() {
 }
 static const void* duo_kernel(const MnlGeom& g) {
   if (g.bsp) {
-    if (g.J == 128) return bsp_ptr<128, 4>();
+    if (g.J == 128) {
+      switch (g.du_nw) {
+        case 4: return bsp_ptr<128, 4>();
+        case 6: return bsp_ptr<128, 6>();
+        case 8: return bsp_ptr<128, 8>();
+        default: return nullptr;
+      }
+    }
     switch (g.du_nw) {
       case 2: return bsp_ptr<64, 2>();
       case 3: return bsp_ptr<64, 3>();
@@ -1028,9 +1038,11 @@ void mnl_duo_geom(MnlGeom* g) {
   if (g->C > kMnlCMax || g->smask != 15 || (g->J != 64 && g->J != 128)) return;
   // compiled shapes: the rank-block body takes a 32 KiB sample as (128, 64) or (64, 128) (two
   // 64-row blocks, 8 LDS-DMA groups per wave, chunk swizzle q ^ (i & 15)); the split body takes
-  // those and every (32 NW, 64) sample, NW = 2..8 (one wave per 32 rows, 8 / NW workgroups per CU)
+  // those, every (32 NW, 64) sample with NW = 2..8 (one wave per 32 rows) and every (16 NW, 128)
+  // sample with NW = 4, 6, 8 (one wave per 16 rows); 8 / NW workgroups per CU
   const bool s32k = g->full && g->I * g->J == 8192;
-  const bool wide = g->J == 64 && g->I % 32 == 0 && g->I / 32 >= 2 && g->I / 32 <= 8;
+  const bool wide = (g->J == 64 && g->I % 32 == 0 && g->I / 32 >= 2 && g->I / 32 <= 8) ||
+                    (g->J == 128 && g->I % 32 == 0 && g->I / 16 >= 4 && g->I / 16 <= 8);
   // form: the f32 rank-block body where it fits (R in 5..8: two rank blocks), the bf16-split body
   // for R <= 4 and for the other (I, 64) shapes; TR_DUO_SPLIT=1 takes the split body for R <= 8,
   // =0 the rank-block body only.  (With the non-temporal sample DMA both run at the same rate at
@@ -1042,7 +1054,7 @@ void mnl_duo_geom(MnlGeom* g) {
   const bool rankblock = s32k && g->nrb == 2;
   const bool bsp = (s32k || wide) && g->R <= 8 && !no_split && (force_split || !rankblock);
   if (!bsp && !rankblock) return;
-  const int nw = bsp && g->J == 64 ? g->I / 32 : 4;
+  const int nw = !bsp ? 4 : g->J == 64 ? g->I / 32 : g->I / 16;
   const int wpc = 8 / nw;
   const int64_t spf = (int64_t)g->I * g->J;
   int64_t o = 2 * spf;  // ring of two samples
@@ -1116,7 +1128,12 @@ hipError_t launch_mnl_duo(const MnlGeom& g, int grid, const float* X, int64_t N,
 #define TR_BSP_LAUNCH(JT, NW) \
   hipLaunchKernelGGL((k_mnl_bsp<JT, NW>), dim3(grid), dim3(NW * TR_WAVE), lds, st, g, a, lab, class_w, stop)
     if (g.J == 128) {
-      TR_BSP_LAUNCH(128, 4);
+      switch (g.du_nw) {
+        case 4: TR_BSP_LAUNCH(128, 4); break;
+        case 6: TR_BSP_LAUNCH(128, 6); break;
+        case 8: TR_BSP_LAUNCH(128, 8); break;
+        default: return hipErrorInvalidValue;
+      }
     } else {
       switch (g.du_nw) {
         case 2: TR_BSP_LAUNCH(64, 2); break;

@@ -117,17 +117,18 @@ def test_linear_full_size_vs_fp64(cfg):
     assert errs["bias"] <= 1e-5, errs  # a sum of signed residuals (measured <= 1e-6)
 
 
-@pytest.mark.parametrize("form", ["bf16split", "rankblock", "fused", "wide64", "wide256"])
+@pytest.mark.parametrize("form", ["bf16split", "rankblock", "fused", "wide64", "wide256", "wide128x128"])
 def test_multinomial_full_size_vs_fp64(form, monkeypatch):
     """Config 3: X (65536, 128, 64), 10 classes, rank 8 (the factored single pass: two 4-wave
     workgroups per CU in the f32 rank-block form (default) and the bf16-split form
-    (TR_DUO_SPLIT=1); with TR_MNL_DUO=0 one 8-wave workgroup per CU).  wide64 / wide256: the
-    split body on (64, 64) samples (2 waves, 4 workgroups per CU) and on (256, 64) samples (8
-    waves, one workgroup per CU, a shape k_mnl_fused does not fit) at the same sample bytes per
-    GPU.  Bars: GRAD_TOL normwise, and no further from fp64 than the reference's own op sequence
+    (TR_DUO_SPLIT=1); with TR_MNL_DUO=0 one 8-wave workgroup per CU).  wide64 / wide256 /
+    wide128x128: the split body on (64, 64) samples (2 waves, 4 workgroups per CU), on (256, 64)
+    samples (8 waves, one workgroup per CU, a shape k_mnl_fused does not fit) and on (128, 128)
+    samples (8 waves of 16 rows) at the same sample bytes per GPU.  Bars: GRAD_TOL normwise, and no further from fp64 than the reference's own op sequence
     in fp32 on the host CPU (the oracle, same factors) is, x2 + 1e-7.  Measured (r05, worst
-    gradient): rank-block 3.1e-7, split 7.2e-7, wide64 3.0e-7, wide256 1.47e-6; the reference in
-    fp32 4.0e-6 (c3), 3.2e-6 (wide64), 9.8e-6 (wide256)."""
+    gradient): rank-block 3.1e-7, split 7.2e-7, wide64 3.0e-7, wide256 1.47e-6, wide128x128
+    1.53e-6; the reference in fp32 4.0e-6 (c3), 3.2e-6 (wide64), 9.8e-6 (wide256), 1.03e-5
+    (wide128x128)."""
     from tensor_regression_amd import CP_logistic_regression
     duo = form != "fused"
     monkeypatch.delenv("TR_DUO_SPLIT", raising=False)
@@ -138,8 +139,8 @@ def test_multinomial_full_size_vs_fp64(form, monkeypatch):
         monkeypatch.setenv("TR_DUO_SPLIT", "1")
     N, I, J, C, R = 65536, 128, 64, 10, 8
     if form.startswith("wide"):
-        I = int(form[4:])
-        N = 65536 * 128 // I
+        I, J = (int(form[4:]), 64) if "x" not in form else (int(v) for v in form[4:].split("x"))
+        N = 65536 * 128 * 64 // (I * J)
     gen = torch.Generator(device=DEV).manual_seed(1234)
     X = torch.randn((N, I, J), device=DEV, generator=gen)
     gc = torch.Generator().manual_seed(99)
@@ -156,7 +157,8 @@ def test_multinomial_full_size_vs_fp64(form, monkeypatch):
     assert "mnl-fused-1pass" in plan.describe
     assert (" duo " in plan.describe) == duo, plan.describe
     if form.startswith("wide"):
-        assert "form=bf16split" in plan.describe and f"waves={I // 32} " in plan.describe, plan.describe
+        nw = I // 32 if J == 64 else I // 16
+        assert "form=bf16split" in plan.describe and f"waves={nw} " in plan.describe, plan.describe
     elif duo:
         assert f"form={form}" in plan.describe, plan.describe
     cw = np.ones(C, np.float32)

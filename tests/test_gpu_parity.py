@@ -367,10 +367,15 @@ def test_linear_sweep_vs_oracle(shape, rank, kind):
                                    atol=RTOL * np.abs(ref["y_hat"]).max())
 
 
-# (shape, C, rank) of the split body's (32 NW, 64) sample shapes: one per wave count, a rank-8
-# model on two rank blocks, fewer samples than workgroups, one rank
+# (shape, C, rank) of the split body's (32 NW, 64) and (16 NW, 128) sample shapes: one per wave
+# count, a rank-8 model on two rank blocks, fewer samples than workgroups, one rank
 WIDE_SHAPES = [((300, 64, 64), 10, 8), ((200, 96, 64), 7, 3), ((400, 128, 64), 5, 2), ((90, 160, 64), 4, 8),
-               ((33, 192, 64), 12, 4), ((60, 224, 64), 3, 6), ((150, 256, 64), 16, 5), ((5, 64, 64), 2, 1)]
+               ((33, 192, 64), 12, 4), ((60, 224, 64), 3, 6), ((150, 256, 64), 16, 5), ((5, 64, 64), 2, 1),
+               ((120, 96, 128), 6, 7), ((80, 128, 128), 10, 8), ((7, 128, 128), 3, 2)]
+
+
+def _split_waves(I, J):
+    return I // 32 if J == 64 else I // 16
 MNL_SHAPES = [((50, 8, 4), 2, 2), ((200, 16, 8), 10, 4), ((97, 5, 7), 16, 3), ((64, 33), 3, 1),
               ((128, 4, 4, 4), 5, 6), ((333, 32, 32), 10, 8), ((40, 64), 16, 2), ((3, 32), 3, 2),
               # factored single pass: ragged 64-blocks, R % 4 != 0, k ranges split over 2 blocks,
@@ -397,11 +402,12 @@ def test_multinomial_sweep_vs_oracle(shape, C, rank, kind):
 
 @pytest.mark.parametrize("shape,C,rank", WIDE_SHAPES)
 def test_multinomial_wide_split_body_selected(shape, C, rank):
-    """(32 NW, 64) samples with R <= 8 take the split body with NW waves per workgroup by default
-    (describe 'form=bf16split waves=NW'); the results are the sweep's."""
+    """(32 NW, 64) and (16 NW, 128) samples with R <= 8 take the split body with NW waves per
+    workgroup by default (describe 'form=bf16split waves=NW'); the results are the sweep's."""
     with path("auto"):
         desc = _multinomial_sweep(shape, C, rank)
-    assert "form=bf16split" in desc and f"waves={shape[1] // 32} wg/cu={8 // (shape[1] // 32)} " in desc, desc
+    nw = _split_waves(shape[1], shape[2])
+    assert "form=bf16split" in desc and f"waves={nw} wg/cu={8 // nw} " in desc, desc
 
 
 def _multinomial_sweep(shape, C, rank):
