@@ -49,6 +49,7 @@ struct MnlGeom {
   // waves per workgroup and workgroups per CU of the two-workgroups-per-CU family (4, 2; the
   // split body on (32 NW, 64) and (16 NW, 128) samples: NW, 8 / NW)
   int du_nw, du_wpc;
+  int du_ns;  // split body: samples in the LDS ring (2; 3 at NW = 5, 6)
   // k_mnl_fused fits this shape (mnl_geom_init may accept a shape only the split body runs)
   int fused_ok;
 };

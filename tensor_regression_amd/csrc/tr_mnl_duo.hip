@@ -617,7 +617,7 @@ __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, cons
 // wave's i k-step, and dPhi1 = sum_n Wv_n V_n is linear in it: the waves' partials are summed
 // once, at the end.  Every wave runs the softmax epilogue of the previous sample (staged between
 // its GEMM steps) for all 8 ranks; wave 0 alone accumulates dPhiC and the loss.
-template <int JT, int NW>
+template <int JT, int NW, int NS>
 __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, const int64_t* __restrict__ lab,
                                          const float* __restrict__ class_w, float* lds, const int wv, const int lane) {
   const int t = threadIdx.x;
@@ -629,7 +629,10 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
   constexpr int NKS = I / 32;           // V k-steps (J = 128: NW / 2 of them, two chunk groups each)
   constexpr int NKT = J / 32;  // T k-steps (j)
   const int R = g.R, C = g.C;
-  float* sU = lds + g.bs_oU;  // [2 parity][NW waves][8 ranks] U partials
+  // NS = 3: a ring of three samples (the DMA of sample k + 2 goes into the slot of k - 1 while k
+  // is computed: two samples in flight), where three fit the workgroup's LDS share
+  static_assert(NS == 2 || (NS == 3 && !TIF), "ring of two (optionally TIF) or three slots");
+  float* sU = lds + g.bs_oU;  // [NS slots][NW waves][8 ranks] U partials
   const float* P0 = a.phi;
   const float* P1 = a.phi + g.offP1;
   const float* PC = a.phi + g.offPC;
@@ -689,7 +692,7 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
   for (int r = 0; r < 8; ++r) pc[r] = (cok && r < R) ? a.w[r] * PC[c * R + r] : 0.f;
   const float pcg0 = pc[gq & 3], pcg1 = pc[4 + (gq & 3)];
   const float wg0 = gq < R ? a.w[gq] : 0.f, wg1 = gq + 4 < R ? a.w[gq + 4] : 0.f;
-  for (int e = t; e < 2 * NW * 8; e += NT_) sU[e] = 0.f;
+  for (int e = t; e < NS * NW * 8; e += NT_) sU[e] = 0.f;
 
   // LDS-DMA map (as the rank-block form): wave wv issues the 1 KiB groups wv + NW gi of every sample
   uint32_t goff[8];
@@ -821,7 +824,7 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
   // holds its operands of k in registers (a second barrier per sample); the kernel is bound by the
   // bytes in flight per CU, not by its issue stream (no-LDS-DMA ablation: 0.256 vs 0.368 ms at c3)
   if (nr > 0) dma_sample(src_of(0), 0);
-  if (nr > 0 && TIF) dma_sample(src_of(nr > 1 ? 1 : 0), 1);
+  if (nr > 0 && (TIF || NS == 3)) dma_sample(src_of(nr > 1 ? 1 : 0), 1);
   int64_t yN = nr > 0 ? lab[sample_of(0)] : 0;
 #if TR_DUO_PROFILE
   unsigned long long prof[4] = {0, 0, 0, 0};
@@ -833,7 +836,7 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
     const int64_t yC = yN;
     const bool more = k + 1 < nr;
     if (!(TR_DUO_SKIP & 16)) yN = lab[sample_of(more ? k + 1 : k)];
-    if (TIF)
+    if (TIF || NS == 3)
       asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // own pieces of k (those of k + 1 may be in flight)
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -842,10 +845,11 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
     TR_DUO_MARK(1);
     const float cwC = du_rdl(cwl, (int)yC);
     // sample k + 2 into this slot once it is read (past the end: a harmless refill of a valid sample)
-    const int kd = TIF ? k + 2 : k + 1;  // the sample this iteration's DMA brings in
+    const int kd = TIF ? k + 2 : k + NS - 1;  // the sample this iteration's DMA brings in
+    constexpr int PS = (SL + NS - 1) % NS;     // slot of sample k - 1 (and of the DMA's target)
     const float* psrc = (kd < nr && !(TR_DUO_SKIP & 1)) ? src_of(kd) : src_of(nr - 1);
-    const uint32_t pm0 = lbase + (uint32_t)((TIF ? SL : SL ^ 1) * 4 * SPF) + (uint32_t)wv * 1024u;
-    epi(0, SL ^ 1, yP, cwP);
+    const uint32_t pm0 = lbase + (uint32_t)((TIF ? SL : PS) * 4 * SPF) + (uint32_t)wv * 1024u;
+    epi(0, PS, yP, cwP);
     const float* sb = lds + SL * SPF;
     du_f32x4 aT[NT], aV[4];
 #pragma unroll
@@ -895,7 +899,7 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
         aV[tv] = bs_mfma(x1, bV3, aV[tv]);
         aV[tv] = bs_mfma(x1, bV12, aV[tv]);
       }
-      if (st >= 1 && st <= 7) epi(st, SL ^ 1, yP, cwP);
+      if (st >= 1 && st <= 7) epi(st, PS, yP, cwP);
       if (SB) __builtin_amdgcn_sched_barrier(0);
     }
     TR_DUO_MARK(2);
@@ -922,9 +926,10 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
     cwP = cwC;
     TR_DUO_MARK(3);
   };
-  for (int k = 0; k < nr; k += 2) {
+  for (int k = 0; k < nr; k += NS) {
     iter(std::integral_constant<int, 0>(), k);
     if (k + 1 < nr) iter(std::integral_constant<int, 1>(), k + 1);
+    if (NS == 3 && k + 2 < nr) iter(std::integral_constant<int, NS == 3 ? 2 : 0>(), k + 2);
   }
 #if TR_DUO_PROFILE
   if (lane == 0 && blockIdx.x < 512)
@@ -934,7 +939,7 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
   du_barrier();  // U partials of the last sample
   if (nr > 0) {
 #pragma unroll
-    for (int st = 0; st < 8; ++st) epi(st, (nr - 1) & 1, yP, cwP);
+    for (int st = 0; st < 8; ++st) epi(st, (nr - 1) % NS, yP, cwP);
   }
 
   // ---- fixed-order reduction into an LDS image of the arena (wave order), slab ----
@@ -974,8 +979,8 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
 }
 
 // NW waves per workgroup, 8 / NW workgroups per CU (the second bound is waves per SIMD: two,
-// 256 VGPRs each)
-template <int JT, int NW>
+// 256 VGPRs each), a ring of NS samples
+template <int JT, int NW, int NS>
 __global__ __launch_bounds__(NW * TR_WAVE, 2) void k_mnl_bsp(MnlGeom g, DuArgs a, const int64_t* __restrict__ lab,
                                                                const float* __restrict__ class_w,
                                                                const int32_t* __restrict__ stop) {
@@ -983,7 +988,7 @@ __global__ __launch_bounds__(NW * TR_WAVE, 2) void k_mnl_bsp(MnlGeom g, DuArgs a
   if (stop != nullptr && *stop != 0) return;
   const int lane = threadIdx.x & (TR_WAVE - 1);
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / TR_WAVE);
-  bsp_body<JT, NW>(g, a, lab, class_w, lds, wv, lane);
+  bsp_body<JT, NW, NS>(g, a, lab, class_w, lds, wv, lane);
 }
 
 template <int JT>
@@ -999,31 +1004,18 @@ __global__ __launch_bounds__(DU_T, 2) void k_mnl_duo(MnlGeom g, DuArgs a, const 
 // ------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------
-// the split body's instantiations: (32 NW, 64) samples with NW = 2..8 waves, (64, 128) with four
-template <int JT, int NW>
-static const void* bsp_ptr() {
-  return reinterpret_cast<const void*>(&k_mnl_bsp<JT, NW>);
-}
+// the split body's instantiations (J, NW, ring slots): (32 NW, 64) samples with NW = 2..8, (16 NW,
+// 128) with NW = 4, 6, 8; a ring of three at NW = 5, 6
+#define TR_BSP_LIST(X) \
+  X(64, 2, 2) X(64, 3, 2) X(64, 4, 2) X(64, 5, 2) X(64, 5, 3) X(64, 6, 2) X(64, 6, 3) X(64, 7, 2) \
+  X(64, 8, 2) X(128, 4, 2) X(128, 6, 2) X(128, 6, 3) X(128, 8, 2)
 static const void* duo_kernel(const MnlGeom& g) {
   if (g.bsp) {
-    if (g.J == 128) {
-      switch (g.du_nw) {
-        case 4: return bsp_ptr<128, 4>();
-        case 6: return bsp_ptr<128, 6>();
-        case 8: return bsp_ptr<128, 8>();
-        default: return nullptr;
-      }
-    }
-    switch (g.du_nw) {
-      case 2: return bsp_ptr<64, 2>();
-      case 3: return bsp_ptr<64, 3>();
-      case 4: return bsp_ptr<64, 4>();
-      case 5: return bsp_ptr<64, 5>();
-      case 6: return bsp_ptr<64, 6>();
-      case 7: return bsp_ptr<64, 7>();
-      case 8: return bsp_ptr<64, 8>();
-      default: return nullptr;
-    }
+#define TR_BSP_PTR(J_, NW_, NS_) \
+  if (g.J == J_ && g.du_nw == NW_ && g.du_ns == NS_) return reinterpret_cast<const void*>(&k_mnl_bsp<J_, NW_, NS_>);
+    TR_BSP_LIST(TR_BSP_PTR)
+#undef TR_BSP_PTR
+    return nullptr;
   }
   return g.J == 64 ? reinterpret_cast<const void*>(&k_mnl_duo<64>) : reinterpret_cast<const void*>(&k_mnl_duo<128>);
 }
@@ -1033,6 +1025,7 @@ void mnl_duo_geom(MnlGeom* g) {
   g->bsp = 0;
   g->du_nw = 4;
   g->du_wpc = 2;
+  g->du_ns = 2;
   const char* env = std::getenv("TR_MNL_DUO");
   if (env != nullptr && env[0] == '0') return;
   if (g->C > kMnlCMax || g->smask != 15 || (g->J != 64 && g->J != 128)) return;
@@ -1057,23 +1050,36 @@ void mnl_duo_geom(MnlGeom* g) {
   const int nw = !bsp ? 4 : g->J == 64 ? g->I / 32 : g->I / 16;
   const int wpc = 8 / nw;
   const int64_t spf = (int64_t)g->I * g->J;
-  int64_t o = 2 * spf;  // ring of two samples
-  g->du_oZ = (int)o;
-  o += 2 * 16 * 4;
-  g->du_oP1 = (int)o;
-  o += 8LL * (g->J + 4);
-  o = (o + 3) & ~(int64_t)3;
-  g->du_oPF = (int)o;  // prefetch scratch line (64 dwords, written by every wave, never read)
-  o += TR_WAVE;
-  g->bs_oU = (int)o;  // bsp: [2][NW waves][8 ranks] U partials
-  o += 2 * nw * 8;
-  g->du_oG = g->slab <= 2 * spf ? 0 : (int)o;  // the arena image aliases the drained ring
-  if (g->du_oG) o += g->slab;
-  o = (o + 3) & ~(int64_t)3;
+  // LDS carve of one workgroup with a ring of ns samples (floats)
+  auto carve = [&](int ns) {
+    int64_t o = ns * spf;
+    g->du_oZ = (int)o;
+    o += 2 * 16 * 4;
+    g->du_oP1 = (int)o;
+    o += 8LL * (g->J + 4);
+    o = (o + 3) & ~(int64_t)3;
+    g->du_oPF = (int)o;  // prefetch scratch line (64 dwords, written by every wave, never read)
+    o += TR_WAVE;
+    g->bs_oU = (int)o;  // bsp: [ns][NW waves][8 ranks] U partials
+    o += ns * nw * 8;
+    g->du_oG = g->slab <= ns * spf ? 0 : (int)o;  // the arena image aliases the drained ring
+    if (g->du_oG) o += g->slab;
+    return (o + 3) & ~(int64_t)3;
+  };
+  // the split body at NW = 5, 6 (one workgroup per CU: 80 / 96 KiB in flight with two slots) takes
+  // a ring of three samples: (160, 64) 58.9 -> 61.4 %, (192, 64) 65.4 -> 68.5 %, (96, 128) 65.8 ->
+  // 69.7 % of HBM (tools/mnl_shapes.py, two runs each); at NW = 3 (two workgroups per CU) three
+  // slots measured the same as two.  TR_DUO_RING=2 keeps two.
+  const char* ring = std::getenv("TR_DUO_RING");
+  const bool ring3_ok = bsp && (nw == 5 || nw == 6) && (g->J == 64 || nw == 6) && !(ring != nullptr && ring[0] == '2');
+  int ns = 2;
+  if (ring3_ok && wpc * carve(3) * 4 <= 160 * 1024) ns = 3;
+  const int64_t o = carve(ns);
   if (wpc * o * 4 > 160 * 1024) return;  // wpc workgroups per CU
   g->du_lds_floats = (int)o;
   g->du_nw = nw;
   g->du_wpc = wpc;
+  g->du_ns = ns;
   g->duo = 1;
   g->bsp = bsp ? 1 : 0;
 }
@@ -1107,6 +1113,7 @@ hipError_t mnl_duo_prepare(MnlGeom* g) {
     g->bsp = 0;
     g->du_nw = 4;
     g->du_wpc = 2;
+    g->du_ns = 2;
     e = duo_kernel_ok(*g, &ok);
     if (e != hipSuccess) return e;
     if (ok) return hipSuccess;
@@ -1115,6 +1122,7 @@ hipError_t mnl_duo_prepare(MnlGeom* g) {
   g->bsp = 0;
   g->du_nw = 4;
   g->du_wpc = 2;
+  g->du_ns = 2;
   return hipSuccess;
 }
 
@@ -1125,27 +1133,14 @@ hipError_t launch_mnl_duo(const MnlGeom& g, int grid, const float* X, int64_t N,
   DuArgs a{X, N, xld, phi, w, scale, gpart, dpart, rows_per_wg, reverse};
   const size_t lds = (size_t)g.du_lds_floats * 4;
   if (g.bsp) {
-#define TR_BSP_LAUNCH(JT, NW) \
-  hipLaunchKernelGGL((k_mnl_bsp<JT, NW>), dim3(grid), dim3(NW * TR_WAVE), lds, st, g, a, lab, class_w, stop)
-    if (g.J == 128) {
-      switch (g.du_nw) {
-        case 4: TR_BSP_LAUNCH(128, 4); break;
-        case 6: TR_BSP_LAUNCH(128, 6); break;
-        case 8: TR_BSP_LAUNCH(128, 8); break;
-        default: return hipErrorInvalidValue;
-      }
-    } else {
-      switch (g.du_nw) {
-        case 2: TR_BSP_LAUNCH(64, 2); break;
-        case 3: TR_BSP_LAUNCH(64, 3); break;
-        case 4: TR_BSP_LAUNCH(64, 4); break;
-        case 5: TR_BSP_LAUNCH(64, 5); break;
-        case 6: TR_BSP_LAUNCH(64, 6); break;
-        case 7: TR_BSP_LAUNCH(64, 7); break;
-        case 8: TR_BSP_LAUNCH(64, 8); break;
-        default: return hipErrorInvalidValue;
-      }
-    }
+#define TR_BSP_LAUNCH(J_, NW_, NS_)                                                                      \
+  if (g.J == J_ && g.du_nw == NW_ && g.du_ns == NS_) {                                                   \
+    hipLaunchKernelGGL((k_mnl_bsp<J_, NW_, NS_>), dim3(grid), dim3(NW_ * TR_WAVE), lds, st, g, a, lab, class_w, \
+                       stop);                                                                            \
+    return hipGetLastError();                                                                            \
+  }
+    TR_BSP_LIST(TR_BSP_LAUNCH)
+    return hipErrorInvalidValue;
 #undef TR_BSP_LAUNCH
   } else if (g.J == 64) {
     hipLaunchKernelGGL((k_mnl_duo<64>), dim3(grid), dim3(DU_T), lds, st, g, a, lab, class_w, stop);

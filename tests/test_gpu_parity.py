@@ -400,14 +400,20 @@ def test_multinomial_sweep_vs_oracle(shape, C, rank, kind):
         _multinomial_sweep(shape, C, rank)
 
 
+@pytest.mark.parametrize("ring", ["auto", "2"])
 @pytest.mark.parametrize("shape,C,rank", WIDE_SHAPES)
-def test_multinomial_wide_split_body_selected(shape, C, rank):
+def test_multinomial_wide_split_body_selected(shape, C, rank, ring, monkeypatch):
     """(32 NW, 64) and (16 NW, 128) samples with R <= 8 take the split body with NW waves per
-    workgroup by default (describe 'form=bf16split waves=NW'); the results are the sweep's."""
+    workgroup by default (describe 'form=bf16split waves=NW'), with a ring of three samples at
+    NW = 5, 6 (nbuf=3; TR_DUO_RING=2 keeps two); the results are the sweep's."""
+    monkeypatch.delenv("TR_DUO_RING", raising=False)
+    if ring == "2":
+        monkeypatch.setenv("TR_DUO_RING", "2")
     with path("auto"):
         desc = _multinomial_sweep(shape, C, rank)
     nw = _split_waves(shape[1], shape[2])
-    assert "form=bf16split" in desc and f"waves={nw} wg/cu={8 // nw} " in desc, desc
+    nbuf = 3 if nw in (5, 6) and ring == "auto" else 2
+    assert "form=bf16split" in desc and f"waves={nw} wg/cu={8 // nw} nbuf={nbuf} " in desc, desc
 
 
 def _multinomial_sweep(shape, C, rank):

@@ -19,7 +19,10 @@ from tensor_regression_amd import CP_logistic_regression  # noqa: E402
 
 dev = "cuda:0"
 SHAPES = [((128, 64), 8), ((64, 128), 8), ((128, 64), 3), ((64, 64), 8), ((96, 64), 8), ((160, 64), 8),
-          ((192, 64), 8), ((256, 64), 8), ((64, 64), 3), ((128, 128), 8), ((256, 128), 8)]
+          ((192, 64), 8), ((224, 64), 8), ((256, 64), 8), ((64, 64), 3), ((96, 128), 8), ((128, 128), 8),
+          ((256, 128), 8)]
+if len(sys.argv) > 1:  # a subset: "I,J" arguments (rank 8)
+    SHAPES = [(tuple(int(v) for v in a.split(",")), 8) for a in sys.argv[1:]]
 C = 10
 for (I, J), R in SHAPES:
     N = (1 << 29) // (I * J)
@@ -42,8 +45,8 @@ for (I, J), R in SHAPES:
     alg = N * (4 * I * J + 8)
     path = plan.describe.split(" path=")[1].split()[0]
     form = (f"duo {plan.describe.split('form=')[1].split()[0]} waves={plan.describe.split('waves=')[1].split()[0]}"
-            if " duo " in plan.describe else path)
-    print(f"(N, I, J) = ({N}, {I}, {J}) R={R}: {form:24s} stream kernels {tot:.4f} ms = "
+            f" nbuf={plan.describe.split('nbuf=')[1].split()[0]}" if " duo " in plan.describe else path)
+    print(f"(N, I, J) = ({N}, {I}, {J}) R={R}: {form:32s} stream kernels {tot:.4f} ms = "
           f"{alg / (tot * 1e-3) / 1e12:.2f} TB/s = {alg / (tot * 1e-3) / 8e12 * 100:.1f} % of HBM  {ms}", flush=True)
     del m, X, y
     torch.cuda.empty_cache()
