@@ -488,8 +488,9 @@ def main():
     spectral_case("spec_slice_shape", 44, (40, 256, 129), 2, 8, 8, 1, False, 0.01, adam, 40)
     spectral_case("spec_slice_d100", 45, (32, 256, 100), 3, 3, 5, 1, [True, False, True], 0.02,
                   {'lr': 0.02, 'amsgrad': True}, 30)
-    # full-mantissa X at config 5's sample shape: every split piece of X (x1, x2, x3) of k_spec_slice's
-    # bf16x3 GEMMs carries data; Rn = 12 takes the unpacked-lin form (slsp=2)
+    # full-mantissa X at config 5's sample shape: every split piece of X carries data in k_spec_slice's
+    # bf16-split GEMMs (X in two pieces by default, x1 + x2; in three with TR_SLICE_XPIECES=3); Rn = 12
+    # takes the unpacked-lin form (slsp=2)
     # (learning rates chosen so the reference's own fp32 trajectory stays within 1.1e-6 / 8.8e-7 of
     # its fp64 restatement over the whole horizon: at lr 0.01 this X drives Adam into oscillation
     # and the reference's fp32 run is 9e-6 from fp64, too close to the 1e-5 bar to test against)
