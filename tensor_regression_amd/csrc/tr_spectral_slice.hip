@@ -98,6 +98,11 @@
 #ifndef TR_SLICE_NOSEL
 #define TR_SLICE_NOSEL 1  // epilogue table reads without per-element lane masks (see tab8)
 #endif
+#ifndef TR_SLICE_AHEAD
+#define TR_SLICE_AHEAD 1  // split kernels (with TR_SLICE_BPF): the next sample's pieces of gradient tile q + 1
+                          // go out at tile q (its reads have landed there), a tile earlier
+#endif
+static_assert(!TR_SLICE_AHEAD || TR_SLICE_BPF, "TR_SLICE_AHEAD needs the next tile's reads issued a tile ahead");
 #ifndef TR_SLICE_PROFILE
 #define TR_SLICE_PROFILE 0  // profiling build: per-phase cycle counts of wave 0 of workgroups 0..255
 #endif
@@ -1005,13 +1010,33 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
               const sl_f4& src = v < 2 ? va : vb;
               sl_splitx_m<SL_XP(SP)>(src[2 * (v & 1) + 0], src[2 * (v & 1) + 1], af, v);
             }
-            if (has_next) {
-              asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // tile q's reads landed
-              dma_piece(nn, q, 0);
+            if (TR_SLICE_AHEAD) {
+              // the reads of tile q and (TR_SLICE_BPF) q + 1 have landed at this wait: the next
+              // sample's pieces of tile q + 1 go out now, a tile earlier (tile 0's at q = 0); the
+              // issue order (tiles in order, the tail after tile qt) is the forward's count
+              if (has_next) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                if (q == 0) {
+                  dma_piece(nn, 0, 0);
+                  dma_piece(nn, 0, 1);
+                  if (TAIL_AT && Dt > 0 && qt == 0) dma_tail(nn);
+                }
+                if (q + 1 < ntl) dma_piece(nn, q + 1, 0);
+              }
+              if (!(TR_SLICE_SKIP & 4)) gacc[q][0] = sl_mfma6<SL_XP(SP)>(af, ds, gacc[q][0]);
+              if (has_next && q + 1 < ntl) {
+                dma_piece(nn, q + 1, 1);
+                if (TAIL_AT && Dt > 0 && q + 1 == qt) dma_tail(nn);
+              }
+            } else {
+              if (has_next) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // tile q's reads landed
+                dma_piece(nn, q, 0);
+              }
+              if (!(TR_SLICE_SKIP & 4)) gacc[q][0] = sl_mfma6<SL_XP(SP)>(af, ds, gacc[q][0]);
+              if (has_next) dma_piece(nn, q, 1);
+              if (TAIL_AT && has_next && Dt > 0 && q == qt) dma_tail(nn);
             }
-            if (!(TR_SLICE_SKIP & 4)) gacc[q][0] = sl_mfma6<SL_XP(SP)>(af, ds, gacc[q][0]);
-            if (has_next) dma_piece(nn, q, 1);
-            if (TAIL_AT && has_next && Dt > 0 && q == qt) dma_tail(nn);
             if (!(TR_SLICE_SKIP & 4)) {
               if constexpr (SL_LP(SP))
                 gacc[q][1] = sl_mfma_lp<SL_XP(SP)>(af, dl, gacc[q][1]);

@@ -6,7 +6,7 @@ tag=$1; cfg=$2; wu=$3; shift 3
 OUT=$ROOT/gpurun_out/$tag
 mkdir -p $OUT
 cd $ROOT || exit 1
-for rnd in 1 2; do
+for rnd in ${AB_ROUNDS:-1 2}; do
   for lib in "$@"; do
     nm=$(basename $lib .so)
     if [ "$lib" = default ]; then

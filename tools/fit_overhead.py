@@ -30,7 +30,7 @@ def main():
     args = ap.parse_args()
     cfg = bench.CONFIGS[args.config]
     dev = "cuda:0"
-    X, y = bench.make_data(cfg, 0, dev)
+    X, y = bench.make_data(cfg, cfg["rows"], 0, dev)
     torch.manual_seed(1)
     R = cfg["rank"]
     if cfg["kind"] == "spectral":
