@@ -18,7 +18,14 @@
 // instruction stream; with the DMA removed entirely the bf16-split body below runs in 0.256 ms at
 // config 3 against 0.368 ms with it.  The non-temporal policy on the sample pieces (TR_DUO_NT, as
 // k_mnl_fused and k_linear_fused use) takes 6-7 % off both bodies (rank-block 0.364 -> 0.339 ms);
-// a second sample in flight per workgroup (TR_DUO_2IF) does not help.
+// a second sample in flight per workgroup (TR_DUO_2IF) does not help at config 3 (two 4-wave
+// workgroups per CU already hold 128 KiB in flight).  The split body's one-workgroup-per-CU
+// shapes at 5 and 6 waves (80 / 96 KiB with two slots) do take a ring of three (+3-4 points).
+//
+// Envelope (mnl_duo_geom): the rank-block body at (128, 64) / (64, 128) rank 5..8; the bf16-split
+// body at those shapes rank <= 4 and at every (32 NW, 64) sample (NW = 2..8) and (16 NW, 128)
+// sample (NW = 4, 6, 8) rank <= 8; <= 16 classes.  Other two-mode shapes run k_mnl_fused
+// (tr_mnl.hip) where it fits, else the two-pass kernels (DESIGN.md "Multinomial, round 5").
 //
 // Per sample k of a workgroup: wait own LDS-DMA of k -> barrier -> epilogue of k-1 (Z partials
 // of the 2 A-waves, double softmax, Wv, gradient scaling) -> GEMM of k with the DMA of k+1 into
