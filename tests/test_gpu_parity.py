@@ -371,7 +371,9 @@ def test_linear_sweep_vs_oracle(shape, rank, kind):
 # count, a rank-8 model on two rank blocks, fewer samples than workgroups, one rank
 WIDE_SHAPES = [((300, 64, 64), 10, 8), ((200, 96, 64), 7, 3), ((400, 128, 64), 5, 2), ((90, 160, 64), 4, 8),
                ((33, 192, 64), 12, 4), ((60, 224, 64), 3, 6), ((150, 256, 64), 16, 5), ((5, 64, 64), 2, 1),
-               ((120, 96, 128), 6, 7), ((80, 128, 128), 10, 8), ((7, 128, 128), 3, 2)]
+               ((120, 96, 128), 6, 7), ((80, 128, 128), 10, 8), ((7, 128, 128), 3, 2),
+               # the ring of three with two and three samples per workgroup (256 workgroups)
+               ((512, 192, 64), 5, 8), ((519, 160, 64), 4, 3)]
 
 
 def _split_waves(I, J):
