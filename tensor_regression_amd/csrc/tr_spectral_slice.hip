@@ -534,7 +534,9 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
     const int x = 4 * c4 + lc;  // chunk within the tile (= r & 7)
     const int sp = lsl ^ sl_swz(x);
     int d = dbase + 4 * (sp & 7);
-    d = d < D ? d : 0;  // a column quad past D (D < 128, D % 4 == 0): any valid quad, times zero
+    d = d < D ? d : 0;  // a column quad past D (D < 128): any valid quad, times zero factor rows; a
+                        // quad straddling D reads the next row's first values (zeros past the
+                        // sample, the descriptor's range), times zero rows as well
     return (uint32_t)(((2 * x + (sp >> 3)) * D + d) * 4);
   };
   uint32_t dvo[2];  // (set by the phase that issues pieces)
@@ -1136,7 +1138,12 @@ void spec_slice_geom(SpecGeom* g) {
   if (g->Rn < 1 || g->Rn > 16 || g->Rs < 1 || g->Rs * g->Cc > 16) return;
   if (!(g->Cc == 1 || g->Cc == 2 || g->Cc == 4)) return;
   if (g->W != 2 * SL_ROWS) return;
-  if (g->D < 97 || g->D > 130 || (g->D < 128 && g->D % 4 != 0)) return;  // whole column quads
+  // any D <= 130: columns past D (a partial last quad, whole padded pairs) meet zero phi(A1) /
+  // phi(C1) rows.  Below D = 128 the kernel still runs all four pairs, and yet it beats the
+  // lock-step k_spec_fused at every D measured (tools/spec_shapes.py, W = 256: D = 96 0.57 vs
+  // 2.27 ms, D = 65 0.74 vs 1.97, D = 33 1.35 vs 3.38, D = 9 4.76 vs 7.03 ms per fit_Adam step at
+  // 2 GiB of X)
+  if (g->D < 1 || g->D > 130) return;
   const int Dt = g->D > 128 ? g->D - 128 : 0;
   if (g->NO > 64) return;
   g->slDt = Dt;

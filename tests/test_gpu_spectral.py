@@ -247,7 +247,7 @@ SHAPES = [
     (77, 17, 7, 2, 0, 4, 1, [False, False, False]),       # rank_normal = 0
     (77, 17, 7, 2, 3, 0, 1, [False, False, False]),       # rank_spectral = 0
 ]
-# shapes of the column-slice training kernel (csrc/tr_spectral_slice.hip: W = 256, 97 <= D <= 130,
+# shapes of the column-slice training kernel (csrc/tr_spectral_slice.hip: W = 256, D <= 130,
 # Rn <= 16, Rs * Cc <= 16, Cc in {1, 2, 4}): every variant of its tail rows (D - 128 = 0, 1, 2),
 # masked columns (D < 128) and norm groups
 SLICE_SHAPES = [
@@ -260,6 +260,14 @@ SLICE_SHAPES = [
     (96, 256, 129, 2, 12, 4, 1, [False, False, False]),   # Rn = 12, one tail row
     (80, 256, 100, 3, 16, 4, 1, [False, True, False]),    # Rn = 16, D < 128 (with D >= 129 beyond LDS)
     (64, 256, 130, 2, 9, 2, 3, [True, False, False]),     # Rn = 9, Cc = 4, two tail rows
+    # D < 128 of any residue: a partial last column quad (its columns past D are the next row's
+    # first values, or zeros past the sample, times zero factor rows) and whole padded pairs
+    (90, 256, 101, 2, 8, 8, 1, [False, False, False]),    # D % 4 = 1
+    (70, 256, 127, 2, 8, 8, 1, [True, False, False]),     # D % 4 = 3
+    (100, 256, 96, 3, 8, 4, 1, [False, True, False]),     # the fourth pair's columns all past D
+    (80, 256, 65, 2, 6, 8, 1, [False, False, False]),     # D = 65 (a length-128 rfft)
+    (60, 256, 34, 2, 4, 4, 1, [False, False, True]),      # one pair and two columns of a second
+    (50, 256, 3, 2, 2, 3, 1, [False, False, False]),      # three columns: one partial quad in all
 ]
 # beyond the fused kernel's envelope: the generic path whatever TR_SPEC_GENERIC says
 WIDE_SHAPES = [
@@ -272,7 +280,7 @@ WIDE_SHAPES = [
 
 def _slice_shape(W, D, Rn, Rs, ncd, O):
     """the column-slice kernel's envelope (spec_slice_geom in csrc/tr_spectral_slice.hip)"""
-    ok = (W == 256 and 97 <= D <= 130 and (D >= 128 or D % 4 == 0) and 1 <= Rn <= 16 and Rs >= 1
+    ok = (W == 256 and D <= 130 and 1 <= Rn <= 16 and Rs >= 1
           and Rs * (ncd + 1) <= 16 and ncd + 1 in (1, 2, 4) and O <= 64)
     small = ((max(D, 128) + 3) // 4 * 4) * (Rn + Rs) + O * 33 + 16 + O * (Rn + Rs + 1) + 64
     return ok and (38144 + ((small + 3) & ~3) + 4) * 4 <= 160 * 1024
