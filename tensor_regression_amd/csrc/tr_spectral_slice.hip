@@ -464,8 +464,8 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       const int64_t w = wbase + 4 * s + gq;
-      bf0[s] = i < RC ? Phi0[w * K + Rn + i] : 0.f;
-      bf1[s] = i < Rn ? Phi0[w * K + i] : 0.f;
+      bf0[s] = (i < RC && w < g.W) ? Phi0[w * K + Rn + i] : 0.f;  // rows past W: padding (zero X)
+      bf1[s] = (i < Rn && w < g.W) ? Phi0[w * K + i] : 0.f;
     }
   } else {
     const int cl = SL_LP(SP) ? (i & 7) : i;  // lin column this lane splits
@@ -474,9 +474,11 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
         const int64_t w0 = wbase + 4 * (8 * S + 2 * m) + gq, w1 = w0 + 4;
-        sl_split_m(i < RC ? Phi0[w0 * K + Rn + i] : 0.f, i < RC ? Phi0[w1 * K + Rn + i] : 0.f, bs[S], m);
+        const bool ok0 = w0 < g.W, ok1 = w1 < g.W;  // rows past W: padding (zero X)
+        sl_split_m((i < RC && ok0) ? Phi0[w0 * K + Rn + i] : 0.f, (i < RC && ok1) ? Phi0[w1 * K + Rn + i] : 0.f, bs[S],
+                   m);
         uint32_t h1, h2, h3;
-        sl_split2(cl < Rn ? Phi0[w0 * K + cl] : 0.f, cl < Rn ? Phi0[w1 * K + cl] : 0.f, h1, h2, h3);
+        sl_split2((cl < Rn && ok0) ? Phi0[w0 * K + cl] : 0.f, (cl < Rn && ok1) ? Phi0[w1 * K + cl] : 0.f, h1, h2, h3);
         if constexpr (SL_LP(SP)) {
           bl[S][0][m] = i < 8 ? h1 : h2;
           bl[S][1][m] = i < 8 ? h3 : 0u;
@@ -548,7 +550,8 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
   // the descriptor starts at this wave's half of the sample (row wbase); tile q's rows are at
   // soffset q * tstr, formed inside the piece's statement (hoisted out of the sample loop, the
   // eight tile offsets took SGPRs the kernel does not have: one spill reload per piece)
-  const uint32_t hbytes = (uint32_t)((g.W - wbase) * D * 4), tstr = (uint32_t)(64 * D);
+  // (W < 256: the rows past W read zeros, the descriptor's range; a half wholly past W has none)
+  const uint32_t hbytes = (uint32_t)((g.W > wbase ? g.W - wbase : 0) * D * 4), tstr = (uint32_t)(64 * D);
   auto rsrc_of = [&](int64_t n) {
     const uint64_t a = (uint64_t)(uintptr_t)(X + n * xld + (int64_t)wbase * D);
     const uint64_t au = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(a >> 32)) << 32) |
@@ -574,7 +577,7 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
     } else if (ln < Dt * TR) {  // lane -> (row 128 + lane / TR, w offset lane % TR)
       const int tr = ln / TR, wo = ln - tr * TR;
       const int64_t w = wbase + TR * p + wo;
-      sl_dma4(X + n * xld + w * D + 128 + tr, sTail);
+      sl_dma4(X + n * xld + (w < g.W ? w : 0) * D + 128 + tr, sTail);  // (rows past W: any valid row, times zero)
     }
   };
   // split kernels (TR_SLICE_TAILLAST): the tail goes last, after every tile piece of the sample;
@@ -1137,7 +1140,11 @@ void spec_slice_geom(SpecGeom* g) {
   if (gen != nullptr && gen[0] == '1') return;
   if (g->Rn < 1 || g->Rn > 16 || g->Rs < 1 || g->Rs * g->Cc > 16) return;
   if (!(g->Cc == 1 || g->Cc == 2 || g->Cc == 4)) return;
-  if (g->W != 2 * SL_ROWS) return;
+  // any W <= 256: rows past W read zeros (the descriptor's range) and meet zero Phi0 rows; even
+  // at W = 32 the padded kernel beats the lock-step k_spec_fused (tools/spec_shapes.py: W = 200
+  // 0.60 vs 1.64 ms, W = 128, D = 129 0.84 vs 1.68, W = 64 1.61 vs 3.13, W = 32 3.15 vs 6.07 ms per
+  // step at 2 GiB of X)
+  if (g->W < 1 || g->W > 2 * SL_ROWS) return;
   // any D <= 130: columns past D (a partial last quad, whole padded pairs) meet zero phi(A1) /
   // phi(C1) rows.  Below D = 128 the kernel still runs all four pairs, and yet it beats the
   // lock-step k_spec_fused at every D measured (tools/spec_shapes.py, W = 256: D = 96 0.57 vs

@@ -5,7 +5,7 @@ Same module functions and `CP_linear_regression` class (same arguments, defaults
 factor layouts Bcp_n (I, Rn, 1) and Bcp_c (W, Rs, n_complex_dim+1), (D, Rs, 1), (n_out, Rs, 1),
 `loss_running` semantics), with the fit/predict hot path on gfx950, each sample of X read from
 HBM once per iteration.  Kernel envelope (the plan picks the first that covers the shape):
-  * training at config-5-like shapes — X.shape[1] == 256, X.shape[2] <= 130, rank_normal <= 16,
+  * training with X.shape[1] <= 256, X.shape[2] <= 130 (config 5: 256 x 129), rank_normal <= 16,
     rank_spectral * (n_complex_dim + 1) <= 16,
     n_complex_dim + 1 in {1, 2, 4}, n_out <= 64 — runs the column-slice single pass
     k_spec_slice (csrc/tr_spectral_slice.hip: bf16 split GEMMs on the matrix cores);

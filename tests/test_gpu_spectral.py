@@ -247,7 +247,7 @@ SHAPES = [
     (77, 17, 7, 2, 0, 4, 1, [False, False, False]),       # rank_normal = 0
     (77, 17, 7, 2, 3, 0, 1, [False, False, False]),       # rank_spectral = 0
 ]
-# shapes of the column-slice training kernel (csrc/tr_spectral_slice.hip: W = 256, D <= 130,
+# shapes of the column-slice training kernel (csrc/tr_spectral_slice.hip: W <= 256, D <= 130,
 # Rn <= 16, Rs * Cc <= 16, Cc in {1, 2, 4}): every variant of its tail rows (D - 128 = 0, 1, 2),
 # masked columns (D < 128) and norm groups
 SLICE_SHAPES = [
@@ -268,6 +268,10 @@ SLICE_SHAPES = [
     (80, 256, 65, 2, 6, 8, 1, [False, False, False]),     # D = 65 (a length-128 rfft)
     (60, 256, 34, 2, 4, 4, 1, [False, False, True]),      # one pair and two columns of a second
     (50, 256, 3, 2, 2, 3, 1, [False, False, False]),      # three columns: one partial quad in all
+    # W < 256: rows past W read zeros and meet zero Phi0 rows
+    (90, 200, 129, 2, 8, 8, 1, [False, False, False]),    # the second half partly past W
+    (80, 128, 65, 3, 8, 4, 1, [False, True, False]),      # the second half wholly past W
+    (70, 100, 130, 2, 6, 6, 1, [True, False, False]),     # two tail rows, the first half partly past W
 ]
 # beyond the fused kernel's envelope: the generic path whatever TR_SPEC_GENERIC says
 WIDE_SHAPES = [
@@ -280,7 +284,7 @@ WIDE_SHAPES = [
 
 def _slice_shape(W, D, Rn, Rs, ncd, O):
     """the column-slice kernel's envelope (spec_slice_geom in csrc/tr_spectral_slice.hip)"""
-    ok = (W == 256 and D <= 130 and 1 <= Rn <= 16 and Rs >= 1
+    ok = (W <= 256 and D <= 130 and 1 <= Rn <= 16 and Rs >= 1
           and Rs * (ncd + 1) <= 16 and ncd + 1 in (1, 2, 4) and O <= 64)
     small = ((max(D, 128) + 3) // 4 * 4) * (Rn + Rs) + O * 33 + 16 + O * (Rn + Rs + 1) + 64
     return ok and (38144 + ((small + 3) & ~3) + 4) * 4 <= 160 * 1024
