@@ -24,7 +24,8 @@
 //
 // Envelope (mnl_duo_geom): the rank-block body at (128, 64) / (64, 128) rank 5..8; the bf16-split
 // body at those shapes rank <= 4 and at every (32 NW, 64) sample (NW = 2..8) and (16 NW, 128)
-// sample (NW = 4, 6, 8) rank <= 8; <= 16 classes.  Other two-mode shapes run k_mnl_fused
+// sample (NW = 4, 6, 8) rank <= 8, any other I in 33..256 (J = 64) / 49..128 (J = 128) padded to
+// the next one; <= 16 classes.  Other two-mode shapes run k_mnl_fused
 // (tr_mnl.hip) where it fits, else the two-pass kernels (DESIGN.md "Multinomial, round 5").
 //
 // Per sample k of a workgroup: wait own LDS-DMA of k -> barrier -> epilogue of k-1 (Z partials
@@ -624,7 +625,7 @@ __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, cons
 // wave's i k-step, and dPhi1 = sum_n Wv_n V_n is linear in it: the waves' partials are summed
 // once, at the end.  Every wave runs the softmax epilogue of the previous sample (staged between
 // its GEMM steps) for all 8 ranks; wave 0 alone accumulates dPhiC and the loss.
-template <int JT, int NW, int NS>
+template <int JT, int NW, int NS, bool PAD>
 __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, const int64_t* __restrict__ lab,
                                          const float* __restrict__ class_w, float* lds, const int wv, const int lane) {
   const int t = threadIdx.x;
@@ -636,6 +637,9 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
   constexpr int NKS = I / 32;           // V k-steps (J = 128: NW / 2 of them, two chunk groups each)
   constexpr int NKT = J / 32;  // T k-steps (j)
   const int R = g.R, C = g.C;
+  // PAD: the sample's g.I rows fill only part of the compiled I; rows g.I..I-1 are padding (they read
+  // any valid row of the sample and meet zero Phi0 rows)
+  const int Ir = PAD ? g.I : I;
   // NS = 3: a ring of three samples (the DMA of sample k + 2 goes into the slot of k - 1 while k
   // is computed: two samples in flight), where three fit the workgroup's LDS share
   static_assert(NS == 2 || (NS == 3 && !TIF), "ring of two (optionally TIF) or three slots");
@@ -683,7 +687,8 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
 #pragma unroll
   for (int v = 0; v < 4; ++v) {  // V (Phi0, element e <-> i = iv0 + 8 gq + e)
     const int i = iv0 + 8 * gq + 2 * v;
-    bsplit(rok ? P0[(int64_t)i * R + r8] : 0.f, rok ? P0[(int64_t)(i + 1) * R + r8] : 0.f, bV12[v], bV3[v], hV[v]);
+    bsplit((rok && (!PAD || i < Ir)) ? P0[(int64_t)i * R + r8] : 0.f,
+           (rok && (!PAD || i + 1 < Ir)) ? P0[(int64_t)(i + 1) * R + r8] : 0.f, bV12[v], bV3[v], hV[v]);
   }
   // U weights: T accumulator (lane (n, gq), reg v) = T[it0 + 16 tt + 4 gq + v][n & 7] after the
   // column fold; lanes n >= 8 hold the same values and weigh 0
@@ -692,7 +697,9 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
   for (int tt = 0; tt < NT; ++tt)
 #pragma unroll
     for (int v = 0; v < 4; ++v)
-      phiU[tt][v] = (lo8 && rok) ? P0[(int64_t)(it0 + 16 * tt + 4 * gq + v) * R + r8] : 0.f;
+      phiU[tt][v] = (lo8 && rok && (!PAD || it0 + 16 * tt + 4 * gq + v < Ir))
+                        ? P0[(int64_t)(it0 + 16 * tt + 4 * gq + v) * R + r8]
+                        : 0.f;
   // epilogue weights: pc[r] = w_r PhiC[c][r]; row gq's ranks gq, gq + 4
   float pc[8];
 #pragma unroll
@@ -708,7 +715,8 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
     const int slot = (wv + NW * gi) * TR_WAVE + lane;
     const int i = slot / JQ;
     const int q = slot - i * JQ;
-    goff[gi] = 4u * (uint32_t)(i * J + 4 * (q ^ (i & 15)));
+    // rows past the real I (a padded sample): any valid row of the sample, its data meets zero Phi0 rows
+    goff[gi] = 4u * (uint32_t)(((!PAD || i < Ir) ? i : 0) * J + 4 * (q ^ (i & 15)));
   }
   const uint32_t lbase = (uint32_t)__builtin_amdgcn_readfirstlane(
       (int)(uint32_t)(uintptr_t)((const __attribute__((address_space(3))) float*)lds));
@@ -959,7 +967,8 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
 #pragma unroll
       for (int tt = 0; tt < NT; ++tt)
 #pragma unroll
-        for (int v = 0; v < 4; ++v) sG[(it0 + 16 * tt + 4 * gq + v) * R + r8] += gT[tt][v];
+        for (int v = 0; v < 4; ++v)
+          if (!PAD || it0 + 16 * tt + 4 * gq + v < g.I) sG[(it0 + 16 * tt + 4 * gq + v) * R + r8] += gT[tt][v];
 #pragma unroll
       for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -987,7 +996,7 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
 
 // NW waves per workgroup, 8 / NW workgroups per CU (the second bound is waves per SIMD: two,
 // 256 VGPRs each), a ring of NS samples
-template <int JT, int NW, int NS>
+template <int JT, int NW, int NS, bool PAD>
 __global__ __launch_bounds__(NW * TR_WAVE, 2) void k_mnl_bsp(MnlGeom g, DuArgs a, const int64_t* __restrict__ lab,
                                                                const float* __restrict__ class_w,
                                                                const int32_t* __restrict__ stop) {
@@ -995,7 +1004,7 @@ __global__ __launch_bounds__(NW * TR_WAVE, 2) void k_mnl_bsp(MnlGeom g, DuArgs a
   if (stop != nullptr && *stop != 0) return;
   const int lane = threadIdx.x & (TR_WAVE - 1);
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / TR_WAVE);
-  bsp_body<JT, NW, NS>(g, a, lab, class_w, lds, wv, lane);
+  bsp_body<JT, NW, NS, PAD>(g, a, lab, class_w, lds, wv, lane);
 }
 
 template <int JT>
@@ -1018,13 +1027,33 @@ __global__ __launch_bounds__(DU_T, 2) void k_mnl_duo(MnlGeom g, DuArgs a, const 
   X(64, 8, 2) X(128, 4, 2) X(128, 6, 2) X(128, 6, 3) X(128, 8, 2)
 static const void* duo_kernel(const MnlGeom& g) {
   if (g.bsp) {
-#define TR_BSP_PTR(J_, NW_, NS_) \
-  if (g.J == J_ && g.du_nw == NW_ && g.du_ns == NS_) return reinterpret_cast<const void*>(&k_mnl_bsp<J_, NW_, NS_>);
+#define TR_BSP_PTR(J_, NW_, NS_)                                                                          \
+  if (g.J == J_ && g.du_nw == NW_ && g.du_ns == NS_)                                                      \
+    return g.du_pad ? reinterpret_cast<const void*>(&k_mnl_bsp<J_, NW_, NS_, true>)                        \
+                    : reinterpret_cast<const void*>(&k_mnl_bsp<J_, NW_, NS_, false>);
     TR_BSP_LIST(TR_BSP_PTR)
 #undef TR_BSP_PTR
     return nullptr;
   }
   return g.J == 64 ? reinterpret_cast<const void*>(&k_mnl_duo<64>) : reinterpret_cast<const void*>(&k_mnl_duo<128>);
+}
+
+// LDS carve of one duo-family workgroup with a ring of ns samples of spf floats (sets the offsets,
+// returns the floats)
+static int64_t duo_carve(MnlGeom* g, int nw, int64_t spf, int ns) {
+  int64_t o = ns * spf;
+  g->du_oZ = (int)o;
+  o += 2 * 16 * 4;
+  g->du_oP1 = (int)o;
+  o += 8LL * (g->J + 4);
+  o = (o + 3) & ~(int64_t)3;
+  g->du_oPF = (int)o;  // prefetch scratch line (64 dwords, written by every wave, never read)
+  o += TR_WAVE;
+  g->bs_oU = (int)o;  // bsp: [ns][NW waves][8 ranks] U partials
+  o += ns * nw * 8;
+  g->du_oG = g->slab <= ns * spf ? 0 : (int)o;  // the arena image aliases the drained ring
+  if (g->du_oG) o += g->slab;
+  return (o + 3) & ~(int64_t)3;
 }
 
 void mnl_duo_geom(MnlGeom* g) {
@@ -1033,6 +1062,7 @@ void mnl_duo_geom(MnlGeom* g) {
   g->du_nw = 4;
   g->du_wpc = 2;
   g->du_ns = 2;
+  g->du_pad = 0;
   const char* env = std::getenv("TR_MNL_DUO");
   if (env != nullptr && env[0] == '0') return;
   if (g->C > kMnlCMax || g->smask != 15 || (g->J != 64 && g->J != 128)) return;
@@ -1041,8 +1071,9 @@ void mnl_duo_geom(MnlGeom* g) {
   // those, every (32 NW, 64) sample with NW = 2..8 (one wave per 32 rows) and every (16 NW, 128)
   // sample with NW = 4, 6, 8 (one wave per 16 rows); 8 / NW workgroups per CU
   const bool s32k = g->full && g->I * g->J == 8192;
-  const bool wide = (g->J == 64 && g->I % 32 == 0 && g->I / 32 >= 2 && g->I / 32 <= 8) ||
-                    (g->J == 128 && g->I % 32 == 0 && g->I / 16 >= 4 && g->I / 16 <= 8);
+  // (a sample whose I is not a whole number of wave rows runs padded: its rows past I read any valid
+  // row of the sample and meet zero Phi0 rows)
+  const bool wide = (g->J == 64 && g->I > 32 && g->I <= 256) || (g->J == 128 && g->I > 48 && g->I <= 128);
   // form: the f32 rank-block body where it fits (R in 5..8: two rank blocks), the bf16-split body
   // for R <= 4 and for the other (I, 64) shapes; TR_DUO_SPLIT=1 takes the split body for R <= 8,
   // =0 the rank-block body only.  (With the non-temporal sample DMA both run at the same rate at
@@ -1054,25 +1085,10 @@ void mnl_duo_geom(MnlGeom* g) {
   const bool rankblock = s32k && g->nrb == 2;
   const bool bsp = (s32k || wide) && g->R <= 8 && !no_split && (force_split || !rankblock);
   if (!bsp && !rankblock) return;
-  const int nw = !bsp ? 4 : g->J == 64 ? g->I / 32 : g->I / 16;
+  const int nw = !bsp ? 4 : g->J == 64 ? (g->I + 31) / 32 : 2 * ((g->I + 31) / 32);
   const int wpc = 8 / nw;
-  const int64_t spf = (int64_t)g->I * g->J;
-  // LDS carve of one workgroup with a ring of ns samples (floats)
-  auto carve = [&](int ns) {
-    int64_t o = ns * spf;
-    g->du_oZ = (int)o;
-    o += 2 * 16 * 4;
-    g->du_oP1 = (int)o;
-    o += 8LL * (g->J + 4);
-    o = (o + 3) & ~(int64_t)3;
-    g->du_oPF = (int)o;  // prefetch scratch line (64 dwords, written by every wave, never read)
-    o += TR_WAVE;
-    g->bs_oU = (int)o;  // bsp: [ns][NW waves][8 ranks] U partials
-    o += ns * nw * 8;
-    g->du_oG = g->slab <= ns * spf ? 0 : (int)o;  // the arena image aliases the drained ring
-    if (g->du_oG) o += g->slab;
-    return (o + 3) & ~(int64_t)3;
-  };
+  const int64_t spf = (int64_t)(!bsp ? g->I : g->J == 64 ? 32 * nw : 16 * nw) * g->J;  // LDS floats per (padded) sample
+  auto carve = [&](int ns) { return duo_carve(g, nw, spf, ns); };
   // the split body at NW = 5, 6 (one workgroup per CU: 80 / 96 KiB in flight with two slots) takes
   // a ring of three samples: (160, 64) 58.9 -> 61.4 %, (192, 64) 65.4 -> 68.5 %, (96, 128) 65.8 ->
   // 69.7 % of HBM (tools/mnl_shapes.py, two runs each); at NW = 3 (two workgroups per CU) three
@@ -1087,6 +1103,7 @@ void mnl_duo_geom(MnlGeom* g) {
   g->du_nw = nw;
   g->du_wpc = wpc;
   g->du_ns = ns;
+  g->du_pad = bsp && spf != (int64_t)g->I * g->J ? 1 : 0;
   g->duo = 1;
   g->bsp = bsp ? 1 : 0;
 }
@@ -1116,6 +1133,14 @@ hipError_t mnl_duo_prepare(MnlGeom* g) {
   hipError_t e = duo_kernel_ok(*g, &ok);
   if (e != hipSuccess) return e;
   if (ok) return hipSuccess;
+  if (g->bsp && g->du_ns == 3) {  // a ring of two instead (the three-slot instantiation spills)
+    const int64_t spf = (int64_t)(g->J == 64 ? 32 : 16) * g->du_nw * g->J;
+    g->du_ns = 2;
+    g->du_lds_floats = (int)duo_carve(g, g->du_nw, spf, 2);
+    e = duo_kernel_ok(*g, &ok);
+    if (e != hipSuccess) return e;
+    if (ok) return hipSuccess;
+  }
   if (g->bsp && g->full && g->I * g->J == 8192 && g->nrb == 2) {  // the rank-block form instead
     g->bsp = 0;
     g->du_nw = 4;
@@ -1130,6 +1155,7 @@ hipError_t mnl_duo_prepare(MnlGeom* g) {
   g->du_nw = 4;
   g->du_wpc = 2;
   g->du_ns = 2;
+  g->du_pad = 0;
   return hipSuccess;
 }
 
@@ -1140,11 +1166,15 @@ hipError_t launch_mnl_duo(const MnlGeom& g, int grid, const float* X, int64_t N,
   DuArgs a{X, N, xld, phi, w, scale, gpart, dpart, rows_per_wg, reverse};
   const size_t lds = (size_t)g.du_lds_floats * 4;
   if (g.bsp) {
-#define TR_BSP_LAUNCH(J_, NW_, NS_)                                                                      \
-  if (g.J == J_ && g.du_nw == NW_ && g.du_ns == NS_) {                                                   \
-    hipLaunchKernelGGL((k_mnl_bsp<J_, NW_, NS_>), dim3(grid), dim3(NW_ * TR_WAVE), lds, st, g, a, lab, class_w, \
-                       stop);                                                                            \
-    return hipGetLastError();                                                                            \
+#define TR_BSP_LAUNCH(J_, NW_, NS_)                                                                       \
+  if (g.J == J_ && g.du_nw == NW_ && g.du_ns == NS_) {                                                    \
+    if (g.du_pad)                                                                                         \
+      hipLaunchKernelGGL((k_mnl_bsp<J_, NW_, NS_, true>), dim3(grid), dim3(NW_ * TR_WAVE), lds, st, g, a, lab, \
+                         class_w, stop);                                                                  \
+    else                                                                                                  \
+      hipLaunchKernelGGL((k_mnl_bsp<J_, NW_, NS_, false>), dim3(grid), dim3(NW_ * TR_WAVE), lds, st, g, a, lab, \
+                         class_w, stop);                                                                  \
+    return hipGetLastError();                                                                             \
   }
     TR_BSP_LIST(TR_BSP_LAUNCH)
     return hipErrorInvalidValue;
