@@ -198,9 +198,12 @@ __global__ __launch_bounds__(T) void k_linear_fused(
   const int wv = t / TR_WAVE;
   float* red = reinterpret_cast<float*>(lds_b + T * CH);  // [2][NW]
 
+  // P may fall short of 4 T CH (a padded row): the float4s past P take zero B, read zero X (the row
+  // descriptor's range) and are not written back
   const float4* B4 = reinterpret_cast<const float4*>(B);
+  const int64_t P4 = P / 4;
 #pragma unroll
-  for (int c = 0; c < CH; ++c) lds_b[t + c * T] = B4[t + c * T];
+  for (int c = 0; c < CH; ++c) lds_b[t + c * T] = t + c * T < P4 ? B4[t + c * T] : make_float4(0.f, 0.f, 0.f, 0.f);
   __syncthreads();
 
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_wg;
@@ -266,7 +269,8 @@ __global__ __launch_bounds__(T) void k_linear_fused(
 
   float4* gp = reinterpret_cast<float4*>(gpart + (int64_t)blockIdx.x * P) + t;
 #pragma unroll
-  for (int c = 0; c < CH; ++c) gp[c * T] = g[c];
+  for (int c = 0; c < CH; ++c)
+    if (t + c * T < P4) gp[c * T] = g[c];
   if (t == 0) {
     dpart[2 * blockIdx.x + 0] = sse;
     dpart[2 * blockIdx.x + 1] = rsum;
@@ -1094,7 +1098,8 @@ hipError_t launch_build_dense(const FactorSet& fs, const float* params, float be
 }
 
 // ---- fused linear --------------------------------------------------------------------------
-// Instantiated (T, CH) pairs: every P = 4*T*CH whose B fits LDS (P <= 40704 floats).
+// Instantiated (T, CH) pairs: every P = 4*T*CH whose B fits LDS (P <= 40704 floats); a P % 4 == 0
+// between them runs the next pair up, padded (choose_fused in tr_api.hip).
 #define TR_FUSED_LIST(X) \
   X(64, 1) X(64, 2) X(64, 3) X(64, 4) X(64, 5) X(64, 6) X(64, 7) X(64, 8) X(64, 12) X(64, 16)           \
   X(128, 1) X(128, 2) X(128, 3) X(128, 4) X(128, 5) X(128, 6) X(128, 7) X(128, 8) X(128, 12) X(128, 16) \
@@ -1107,7 +1112,8 @@ static hipError_t fused_launch_t(int grid, const float* X, int64_t N, int64_t P,
                                  const float* bias, const float* y, float scale, float* gpart,
                                  double* dpart, float* yhat, int64_t rpw, int reverse,
                                  const int32_t* stop, hipStream_t st) {
-  const size_t lds = (size_t)P * sizeof(float) + 2 * (T / TR_WAVE) * sizeof(float);
+  const size_t lds = (size_t)T * CH * 4 * sizeof(float) + 2 * (T / TR_WAVE) * sizeof(float);  // B padded to 4 T CH
+  if (P > 4 * (int64_t)T * CH) return hipErrorInvalidValue;
   hipLaunchKernelGGL((k_linear_fused<T, CH>), dim3(grid), dim3(T), lds, st, X, N, P, xld, B, bias, y,
                      scale, gpart, dpart, yhat, rpw, reverse, stop);
   return hipGetLastError();

@@ -331,7 +331,29 @@ LIN_SHAPES = [
     ((2, 200, 332), 4),        # N < number of clusters: most clusters own no rows
     ((90, 10, 10), 65),        # rank beyond 64: MTTKRP rank tiles of 64
     ((50, 6, 5, 4), 200),      # 4 rank tiles, 3 feature modes
+    # P % 4 == 0 without an exact 4 T CH: the fused pass over rows padded to the next instantiated
+    # width (the padded float4s read zeros past the row descriptor's range and hold zero B)
+    ((200, 100, 100), 4),      # P = 10000 -> T = 512, CH = 5 (2.4 % padding)
+    ((150, 160, 160), 8),      # P = 25600 -> T = 1024, CH = 7
+    ((90, 250, 130), 3),       # P = 32500 -> T = 1024, CH = 8 (0.8 %)
 ]
+PADDED_FUSED = [((200, 100, 100), 4), ((150, 160, 160), 8), ((90, 250, 130), 3)]
+
+
+@pytest.mark.parametrize("shape,rank", PADDED_FUSED)
+def test_linear_padded_rows_take_the_fused_pass(shape, rank):
+    """shapes whose P has no exact 4 T CH factorisation run the fused single pass (T, CH with at
+    most 25 % padding) instead of the two-pass kernels or a 2-slice cluster; the sweep above checks
+    their numbers against the oracle"""
+    from tensor_regression_amd import CP_linear_regression
+    with path("auto"):
+        X = torch.zeros(*shape, device=DEV)
+        model = CP_linear_regression(X.shape, rank=rank, device=DEV)
+        plan = model._get_plan(X, shape[0])
+        P = int(np.prod(shape[1:]))
+        T = int(plan.describe.split(" T=")[1].split()[0])
+        CH = int(plan.describe.split(" CH=")[1].split()[0])
+        assert "path=fused-1pass" in plan.describe and P <= 4 * T * CH <= 1.25 * P, plan.describe
 
 
 @pytest.mark.parametrize("kind", ["auto", "twopass"])
