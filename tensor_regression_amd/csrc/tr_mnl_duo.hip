@@ -24,8 +24,8 @@
 //
 // Envelope (mnl_duo_geom): the rank-block body at (128, 64) / (64, 128) rank 5..8; the bf16-split
 // body at those shapes rank <= 4 and at every (32 NW, 64) sample (NW = 2..8) and (16 NW, 128)
-// sample (NW = 4, 6, 8) rank <= 8, any other I in 33..256 (J = 64) / 49..128 (J = 128) padded to
-// the next one; <= 16 classes.  Other two-mode shapes run k_mnl_fused
+// sample (NW = 4, 6, 8) rank <= 8, any other I in 33..256 / 49..128 and J % 4 == 0 in 36..128
+// padded to the next of those shapes; <= 16 classes.  Other two-mode shapes run k_mnl_fused
 // (tr_mnl.hip) where it fits, else the two-pass kernels (DESIGN.md "Multinomial, round 5").
 //
 // Per sample k of a workgroup: wait own LDS-DMA of k -> barrier -> epilogue of k-1 (Z partials
@@ -637,9 +637,9 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
   constexpr int NKS = I / 32;           // V k-steps (J = 128: NW / 2 of them, two chunk groups each)
   constexpr int NKT = J / 32;  // T k-steps (j)
   const int R = g.R, C = g.C;
-  // PAD: the sample's g.I rows fill only part of the compiled I; rows g.I..I-1 are padding (they read
-  // any valid row of the sample and meet zero Phi0 rows)
-  const int Ir = PAD ? g.I : I;
+  // PAD: the sample's g.I x g.J (g.J % 4 == 0) fills only part of the compiled I x J; the padding
+  // rows and column chunks read the sample's first chunk (valid memory) and meet zero Phi0 / Phi1 rows
+  const int Ir = PAD ? g.I : I, Jr = PAD ? g.J : J;
   // NS = 3: a ring of three samples (the DMA of sample k + 2 goes into the slot of k - 1 while k
   // is computed: two samples in flight), where three fit the workgroup's LDS share
   static_assert(NS == 2 || (NS == 3 && !TIF), "ring of two (optionally TIF) or three slots");
@@ -681,8 +681,8 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
       const int j = 32 * s + 8 * gq + 2 * v;
-      bsplit(rok ? P1[(int64_t)j * R + r8] : 0.f, rok ? P1[(int64_t)(j + 1) * R + r8] : 0.f, bT12[s][v], bT3[s][v],
-             hT[s][v]);
+      bsplit((rok && (!PAD || j < Jr)) ? P1[(int64_t)j * R + r8] : 0.f,
+             (rok && (!PAD || j + 1 < Jr)) ? P1[(int64_t)(j + 1) * R + r8] : 0.f, bT12[s][v], bT3[s][v], hT[s][v]);
     }
 #pragma unroll
   for (int v = 0; v < 4; ++v) {  // V (Phi0, element e <-> i = iv0 + 8 gq + e)
@@ -715,8 +715,12 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
     const int slot = (wv + NW * gi) * TR_WAVE + lane;
     const int i = slot / JQ;
     const int q = slot - i * JQ;
-    // rows past the real I (a padded sample): any valid row of the sample, its data meets zero Phi0 rows
-    goff[gi] = 4u * (uint32_t)(((!PAD || i < Ir) ? i : 0) * J + 4 * (q ^ (i & 15)));
+    if (PAD) {  // source offset in the real (Ir x Jr) sample; padding: its first chunk
+      const int cq = q ^ (i & 15);
+      goff[gi] = (i < Ir && 4 * cq < Jr) ? 4u * (uint32_t)(i * Jr + 4 * cq) : 0u;
+    } else {
+      goff[gi] = 4u * (uint32_t)(i * J + 4 * (q ^ (i & 15)));
+    }
   }
   const uint32_t lbase = (uint32_t)__builtin_amdgcn_readfirstlane(
       (int)(uint32_t)(uintptr_t)((const __attribute__((address_space(3))) float*)lds));
@@ -830,10 +834,11 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
     }
   };
 
+  auto dma_piece = [&](uint32_t off, const float* src, uint32_t m0v) { du_dma_s(off, src, m0v); };
   auto dma_sample = [&](const float* src, int slot) {
 #pragma unroll
     for (int gi = 0; gi < 8; ++gi)
-      du_dma_s(goff[gi], src, lbase + (uint32_t)(slot * 4 * SPF) + (uint32_t)(wv + NW * gi) * 1024u);
+      dma_piece(goff[gi], src, lbase + (uint32_t)(slot * 4 * SPF) + (uint32_t)(wv + NW * gi) * 1024u);
   };
   // two samples in flight per workgroup: sample k + 2 goes into slot k & 1 as soon as every wave
   // holds its operands of k in registers (a second barrier per sample); the kernel is bound by the
@@ -886,7 +891,7 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
     if (TIF) du_barrier();  // (its lgkmcnt(0): this wave's reads landed) every wave's operands of k read
 #pragma unroll
     for (int st = 0; st < NU + 4; ++st) {
-      if (!(TR_DUO_SKIP & 8)) du_dma_s(goff[st], psrc, pm0 + (uint32_t)st * (uint32_t)(NW * 1024));
+      if (!(TR_DUO_SKIP & 8)) dma_piece(goff[st], psrc, pm0 + (uint32_t)st * (uint32_t)(NW * 1024));
       sl_u4 x1, x2;
       if (st < NU) {
 #pragma unroll
@@ -974,7 +979,7 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
           const int j = 4 * (cv - n + 4 * gq + v) + q;  // chunk (row 4 gq + v of the tile) -> j = 4 chunk + tile
-          sG[g.offP1 + j * R + r8] += gV[q][v];
+          if (!PAD || j < Jr) sG[g.offP1 + j * R + r8] += gV[q][v];
         }
     }
     if (ws == wv && wv == 0 && cok) {
@@ -1028,7 +1033,7 @@ __global__ __launch_bounds__(DU_T, 2) void k_mnl_duo(MnlGeom g, DuArgs a, const 
 static const void* duo_kernel(const MnlGeom& g) {
   if (g.bsp) {
 #define TR_BSP_PTR(J_, NW_, NS_)                                                                          \
-  if (g.J == J_ && g.du_nw == NW_ && g.du_ns == NS_)                                                      \
+  if (g.du_jt == J_ && g.du_nw == NW_ && g.du_ns == NS_)                                                   \
     return g.du_pad ? reinterpret_cast<const void*>(&k_mnl_bsp<J_, NW_, NS_, true>)                        \
                     : reinterpret_cast<const void*>(&k_mnl_bsp<J_, NW_, NS_, false>);
     TR_BSP_LIST(TR_BSP_PTR)
@@ -1045,7 +1050,7 @@ static int64_t duo_carve(MnlGeom* g, int nw, int64_t spf, int ns) {
   g->du_oZ = (int)o;
   o += 2 * 16 * 4;
   g->du_oP1 = (int)o;
-  o += 8LL * (g->J + 4);
+  o += 8LL * (g->du_jt + 4);
   o = (o + 3) & ~(int64_t)3;
   g->du_oPF = (int)o;  // prefetch scratch line (64 dwords, written by every wave, never read)
   o += TR_WAVE;
@@ -1063,17 +1068,20 @@ void mnl_duo_geom(MnlGeom* g) {
   g->du_wpc = 2;
   g->du_ns = 2;
   g->du_pad = 0;
+  g->du_jt = g->J;
   const char* env = std::getenv("TR_MNL_DUO");
   if (env != nullptr && env[0] == '0') return;
-  if (g->C > kMnlCMax || g->smask != 15 || (g->J != 64 && g->J != 128)) return;
+  if (g->C > kMnlCMax || g->J % 4 != 0 || g->J <= 32 || g->J > 128) return;
+  // the compiled row width: J itself (64, 128) or the next one up (a padded sample)
+  const int jt = g->J <= 64 ? 64 : 128;
   // compiled shapes: the rank-block body takes a 32 KiB sample as (128, 64) or (64, 128) (two
   // 64-row blocks, 8 LDS-DMA groups per wave, chunk swizzle q ^ (i & 15)); the split body takes
   // those, every (32 NW, 64) sample with NW = 2..8 (one wave per 32 rows) and every (16 NW, 128)
   // sample with NW = 4, 6, 8 (one wave per 16 rows); 8 / NW workgroups per CU
-  const bool s32k = g->full && g->I * g->J == 8192;
+  const bool s32k = g->full && g->I * g->J == 8192 && g->smask == 15;
   // (a sample whose I is not a whole number of wave rows runs padded: its rows past I read any valid
   // row of the sample and meet zero Phi0 rows)
-  const bool wide = (g->J == 64 && g->I > 32 && g->I <= 256) || (g->J == 128 && g->I > 48 && g->I <= 128);
+  const bool wide = (jt == 64 && g->I > 32 && g->I <= 256) || (jt == 128 && g->I > 48 && g->I <= 128);
   // form: the f32 rank-block body where it fits (R in 5..8: two rank blocks), the bf16-split body
   // for R <= 4 and for the other (I, 64) shapes; TR_DUO_SPLIT=1 takes the split body for R <= 8,
   // =0 the rank-block body only.  (With the non-temporal sample DMA both run at the same rate at
@@ -1085,16 +1093,17 @@ void mnl_duo_geom(MnlGeom* g) {
   const bool rankblock = s32k && g->nrb == 2;
   const bool bsp = (s32k || wide) && g->R <= 8 && !no_split && (force_split || !rankblock);
   if (!bsp && !rankblock) return;
-  const int nw = !bsp ? 4 : g->J == 64 ? (g->I + 31) / 32 : 2 * ((g->I + 31) / 32);
+  const int nw = !bsp ? 4 : jt == 64 ? (g->I + 31) / 32 : 2 * ((g->I + 31) / 32);
+  g->du_jt = bsp ? jt : g->J;
   const int wpc = 8 / nw;
-  const int64_t spf = (int64_t)(!bsp ? g->I : g->J == 64 ? 32 * nw : 16 * nw) * g->J;  // LDS floats per (padded) sample
+  const int64_t spf = (int64_t)(!bsp ? g->I : jt == 64 ? 32 * nw : 16 * nw) * g->du_jt;  // LDS floats per (padded) sample
   auto carve = [&](int ns) { return duo_carve(g, nw, spf, ns); };
   // the split body at NW = 5, 6 (one workgroup per CU: 80 / 96 KiB in flight with two slots) takes
   // a ring of three samples: (160, 64) 58.9 -> 61.4 %, (192, 64) 65.4 -> 68.5 %, (96, 128) 65.8 ->
   // 69.7 % of HBM (tools/mnl_shapes.py, two runs each); at NW = 3 (two workgroups per CU) three
   // slots measured the same as two.  TR_DUO_RING=2 keeps two.
   const char* ring = std::getenv("TR_DUO_RING");
-  const bool ring3_ok = bsp && (nw == 5 || nw == 6) && (g->J == 64 || nw == 6) && !(ring != nullptr && ring[0] == '2');
+  const bool ring3_ok = bsp && (nw == 5 || nw == 6) && (jt == 64 || nw == 6) && !(ring != nullptr && ring[0] == '2');
   int ns = 2;
   if (ring3_ok && wpc * carve(3) * 4 <= 160 * 1024) ns = 3;
   const int64_t o = carve(ns);
@@ -1134,7 +1143,7 @@ hipError_t mnl_duo_prepare(MnlGeom* g) {
   if (e != hipSuccess) return e;
   if (ok) return hipSuccess;
   if (g->bsp && g->du_ns == 3) {  // a ring of two instead (the three-slot instantiation spills)
-    const int64_t spf = (int64_t)(g->J == 64 ? 32 : 16) * g->du_nw * g->J;
+    const int64_t spf = (int64_t)(g->du_jt == 64 ? 32 : 16) * g->du_nw * g->du_jt;
     g->du_ns = 2;
     g->du_lds_floats = (int)duo_carve(g, g->du_nw, spf, 2);
     e = duo_kernel_ok(*g, &ok);
@@ -1146,6 +1155,7 @@ hipError_t mnl_duo_prepare(MnlGeom* g) {
     g->du_nw = 4;
     g->du_wpc = 2;
     g->du_ns = 2;
+    g->du_jt = g->J;
     e = duo_kernel_ok(*g, &ok);
     if (e != hipSuccess) return e;
     if (ok) return hipSuccess;
@@ -1156,6 +1166,7 @@ hipError_t mnl_duo_prepare(MnlGeom* g) {
   g->du_wpc = 2;
   g->du_ns = 2;
   g->du_pad = 0;
+  g->du_jt = g->J;
   return hipSuccess;
 }
 
@@ -1167,7 +1178,7 @@ hipError_t launch_mnl_duo(const MnlGeom& g, int grid, const float* X, int64_t N,
   const size_t lds = (size_t)g.du_lds_floats * 4;
   if (g.bsp) {
 #define TR_BSP_LAUNCH(J_, NW_, NS_)                                                                       \
-  if (g.J == J_ && g.du_nw == NW_ && g.du_ns == NS_) {                                                    \
+  if (g.du_jt == J_ && g.du_nw == NW_ && g.du_ns == NS_) {                                                 \
     if (g.du_pad)                                                                                         \
       hipLaunchKernelGGL((k_mnl_bsp<J_, NW_, NS_, true>), dim3(grid), dim3(NW_ * TR_WAVE), lds, st, g, a, lab, \
                          class_w, stop);                                                                  \

@@ -398,11 +398,18 @@ WIDE_SHAPES = [((300, 64, 64), 10, 8), ((200, 96, 64), 7, 3), ((400, 128, 64), 5
                ((512, 192, 64), 5, 8), ((519, 160, 64), 4, 3),
                # padded samples: I not a whole number of wave rows (rows past I meet zero Phi0 rows)
                ((300, 100, 64), 10, 8), ((150, 33, 64), 5, 3), ((90, 250, 64), 7, 6), ((80, 70, 128), 4, 8),
-               ((60, 50, 128), 3, 2), ((40, 120, 128), 16, 5)]
+               ((60, 50, 128), 3, 2), ((40, 120, 128), 16, 5),
+               # padded row widths: J % 4 == 0 up to the next 64 / 128 (columns past J meet zero Phi1 rows)
+               ((200, 128, 48), 10, 8), ((150, 64, 96), 5, 3), ((100, 100, 100), 6, 6), ((120, 200, 40), 4, 8),
+               ((80, 40, 60), 3, 2)]
+
+
+def _split_jt(J):
+    return 64 if J <= 64 else 128
 
 
 def _split_waves(I, J):
-    return (I + 31) // 32 if J == 64 else 2 * ((I + 31) // 32)
+    return (I + 31) // 32 if _split_jt(J) == 64 else 2 * ((I + 31) // 32)
 MNL_SHAPES = [((50, 8, 4), 2, 2), ((200, 16, 8), 10, 4), ((97, 5, 7), 16, 3), ((64, 33), 3, 1),
               ((128, 4, 4, 4), 5, 6), ((333, 32, 32), 10, 8), ((40, 64), 16, 2), ((3, 32), 3, 2),
               # factored single pass: ragged 64-blocks, R % 4 != 0, k ranges split over 2 blocks,
@@ -439,9 +446,10 @@ def test_multinomial_wide_split_body_selected(shape, C, rank, ring, monkeypatch)
     with path("auto"):
         desc = _multinomial_sweep(shape, C, rank)
     nw = _split_waves(shape[1], shape[2])
-    padded = shape[1] != (32 if shape[2] == 64 else 16) * nw
+    jt = _split_jt(shape[2])
+    padded = shape[1] != (32 if jt == 64 else 16) * nw or shape[2] != jt
     # (the padded (16 NW, 128) body with a ring of three spills at NW = 6: the plan takes two slots)
-    nbuf = 3 if nw in (5, 6) and ring == "auto" and not (padded and shape[2] == 128) else 2
+    nbuf = 3 if nw in (5, 6) and ring == "auto" and not (padded and jt == 128) else 2
     assert "form=bf16split" in desc and f"waves={nw} wg/cu={8 // nw} nbuf={nbuf} " in desc, desc
 
 
