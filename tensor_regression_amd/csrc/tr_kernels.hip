@@ -198,12 +198,26 @@ __global__ __launch_bounds__(T) void k_linear_fused(
   const int wv = t / TR_WAVE;
   float* red = reinterpret_cast<float*>(lds_b + T * CH);  // [2][NW]
 
-  // P may fall short of 4 T CH (a padded row): the float4s past P take zero B, read zero X (the row
-  // descriptor's range) and are not written back
+  // P may fall short of 4 T CH (a padded row) and need not be a multiple of 4: the floats past P take
+  // zero B and read zero X (the row descriptor's range is checked per dword; rows start 4-B aligned,
+  // which a dwordx4 buffer load takes), and the partial slab is written with a stride of P rounded up
+  // to 4 floats (its floats past P hold zero)
   const float4* B4 = reinterpret_cast<const float4*>(B);
-  const int64_t P4 = P / 4;
+  const int64_t P4 = P / 4, Pq = (P + 3) / 4;
 #pragma unroll
-  for (int c = 0; c < CH; ++c) lds_b[t + c * T] = t + c * T < P4 ? B4[t + c * T] : make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int c = 0; c < CH; ++c) {
+    const int64_t q = t + c * T;
+    float4 b = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (q < P4) {
+      b = B4[q];
+    } else if (q < Pq) {  // the last, partial quad
+      const int64_t e = 4 * q;
+      b.x = B[e];
+      if (e + 1 < P) b.y = B[e + 1];
+      if (e + 2 < P) b.z = B[e + 2];
+    }
+    lds_b[q] = b;
+  }
   __syncthreads();
 
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_wg;
@@ -267,10 +281,10 @@ __global__ __launch_bounds__(T) void k_linear_fused(
     }
   }
 
-  float4* gp = reinterpret_cast<float4*>(gpart + (int64_t)blockIdx.x * P) + t;
+  float4* gp = reinterpret_cast<float4*>(gpart + (int64_t)blockIdx.x * (4 * Pq)) + t;
 #pragma unroll
   for (int c = 0; c < CH; ++c)
-    if (t + c * T < P4) gp[c * T] = g[c];
+    if (t + c * T < Pq) gp[c * T] = g[c];
   if (t == 0) {
     dpart[2 * blockIdx.x + 0] = sse;
     dpart[2 * blockIdx.x + 1] = rsum;
@@ -1098,14 +1112,15 @@ hipError_t launch_build_dense(const FactorSet& fs, const float* params, float be
 }
 
 // ---- fused linear --------------------------------------------------------------------------
-// Instantiated (T, CH) pairs: every P = 4*T*CH whose B fits LDS (P <= 40704 floats); a P % 4 == 0
-// between them runs the next pair up, padded (choose_fused in tr_api.hip).
+// Instantiated (T, CH) pairs: every P = 4*T*CH whose B fits LDS (P <= 40704 floats); any other P
+// runs the next pair up, padded (choose_fused in tr_api.hip; at most 25 % padding).
 #define TR_FUSED_LIST(X) \
   X(64, 1) X(64, 2) X(64, 3) X(64, 4) X(64, 5) X(64, 6) X(64, 7) X(64, 8) X(64, 12) X(64, 16)           \
   X(128, 1) X(128, 2) X(128, 3) X(128, 4) X(128, 5) X(128, 6) X(128, 7) X(128, 8) X(128, 12) X(128, 16) \
   X(256, 1) X(256, 2) X(256, 3) X(256, 4) X(256, 5) X(256, 6) X(256, 7) X(256, 8) X(256, 12) X(256, 16) \
-  X(512, 1) X(512, 2) X(512, 3) X(512, 4) X(512, 5) X(512, 6) X(512, 7) X(512, 8) X(512, 12) X(512, 16) \
-  X(1024, 1) X(1024, 2) X(1024, 3) X(1024, 4) X(1024, 5) X(1024, 6) X(1024, 7) X(1024, 8)
+  X(512, 1) X(512, 2) X(512, 3) X(512, 4) X(512, 5) X(512, 6) X(512, 7) X(512, 8) X(512, 9) X(512, 10)  \
+  X(512, 11) X(512, 12) X(512, 13) X(512, 14) X(512, 15) X(512, 16)                                     \
+  X(1024, 1) X(1024, 2) X(1024, 3) X(1024, 4) X(1024, 5) X(1024, 6) X(1024, 7) X(1024, 8) X(1024, 9)
 
 template <int T, int CH>
 static hipError_t fused_launch_t(int grid, const float* X, int64_t N, int64_t P, int64_t xld, const float* B,
