@@ -1112,15 +1112,16 @@ hipError_t launch_build_dense(const FactorSet& fs, const float* params, float be
 }
 
 // ---- fused linear --------------------------------------------------------------------------
-// Instantiated (T, CH) pairs: every P = 4*T*CH whose B fits LDS (P <= 40704 floats); any other P
-// runs the next pair up, padded (choose_fused in tr_api.hip; at most 25 % padding).
+// Instantiated (T, CH) pairs: every P = 4*T*CH whose B fits LDS (P <= 40704 floats) and whose
+// registers fit (T = 512 spills above CH = 16, T = 1024 at CH = 8: prepare_linear_fused rejects
+// it); any other P runs the next pair up, padded (choose_fused in tr_api.hip; <= 25 % padding).
 #define TR_FUSED_LIST(X) \
   X(64, 1) X(64, 2) X(64, 3) X(64, 4) X(64, 5) X(64, 6) X(64, 7) X(64, 8) X(64, 12) X(64, 16)           \
   X(128, 1) X(128, 2) X(128, 3) X(128, 4) X(128, 5) X(128, 6) X(128, 7) X(128, 8) X(128, 12) X(128, 16) \
   X(256, 1) X(256, 2) X(256, 3) X(256, 4) X(256, 5) X(256, 6) X(256, 7) X(256, 8) X(256, 12) X(256, 16) \
   X(512, 1) X(512, 2) X(512, 3) X(512, 4) X(512, 5) X(512, 6) X(512, 7) X(512, 8) X(512, 9) X(512, 10)  \
   X(512, 11) X(512, 12) X(512, 13) X(512, 14) X(512, 15) X(512, 16)                                     \
-  X(1024, 1) X(1024, 2) X(1024, 3) X(1024, 4) X(1024, 5) X(1024, 6) X(1024, 7) X(1024, 8) X(1024, 9)
+  X(1024, 1) X(1024, 2) X(1024, 3) X(1024, 4) X(1024, 5) X(1024, 6) X(1024, 7) X(1024, 8)
 
 template <int T, int CH>
 static hipError_t fused_launch_t(int grid, const float* X, int64_t N, int64_t P, int64_t xld, const float* B,
