@@ -24,7 +24,7 @@
 //
 // Envelope (mnl_duo_geom): the rank-block body at (128, 64) / (64, 128) rank 5..8; the bf16-split
 // body at those shapes rank <= 4 and at every (32 NW, 64) sample (NW = 2..8) and (16 NW, 128)
-// sample (NW = 4, 6, 8) rank <= 8, any other I in 33..256 / 49..128 and J % 4 == 0 in 36..128
+// sample (NW = 4, 6, 8) rank <= 8, any other I in 33..256 / 49..128 and J % 4 == 0 in 28..128
 // padded to the next of those shapes; <= 16 classes.  Other two-mode shapes run k_mnl_fused
 // (tr_mnl.hip) where it fits, else the two-pass kernels (DESIGN.md "Multinomial, round 5").
 //
@@ -1071,7 +1071,9 @@ void mnl_duo_geom(MnlGeom* g) {
   g->du_jt = g->J;
   const char* env = std::getenv("TR_MNL_DUO");
   if (env != nullptr && env[0] == '0') return;
-  if (g->C > kMnlCMax || g->J % 4 != 0 || g->J <= 32 || g->J > 128) return;
+  // (J from 28 up: padded to 64, J = 32 runs at 46-48 % of HBM against 14-37 % on the fallbacks; at
+  // J = 24 and 16 the two-pass kernels are faster, 34 vs 29 % and 34 vs 25 %, tools/mnl_shapes.py)
+  if (g->C > kMnlCMax || g->J % 4 != 0 || g->J < 28 || g->J > 128) return;
   // the compiled row width: J itself (64, 128) or the next one up (a padded sample)
   const int jt = g->J <= 64 ? 64 : 128;
   // compiled shapes: the rank-block body takes a 32 KiB sample as (128, 64) or (64, 128) (two

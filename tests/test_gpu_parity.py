@@ -402,7 +402,7 @@ WIDE_SHAPES = [((300, 64, 64), 10, 8), ((200, 96, 64), 7, 3), ((400, 128, 64), 5
                ((60, 50, 128), 3, 2), ((40, 120, 128), 16, 5),
                # padded row widths: J % 4 == 0 up to the next 64 / 128 (columns past J meet zero Phi1 rows)
                ((200, 128, 48), 10, 8), ((150, 64, 96), 5, 3), ((100, 100, 100), 6, 6), ((120, 200, 40), 4, 8),
-               ((80, 40, 60), 3, 2)]
+               ((80, 40, 60), 3, 2), ((300, 128, 32), 10, 8), ((200, 64, 28), 4, 3)]
 
 
 def _split_jt(J):
