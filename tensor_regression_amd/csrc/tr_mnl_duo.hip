@@ -1083,7 +1083,9 @@ void mnl_duo_geom(MnlGeom* g) {
   const bool s32k = g->full && g->I * g->J == 8192 && g->smask == 15;
   // (a sample whose I is not a whole number of wave rows runs padded: its rows past I read any valid
   // row of the sample and meet zero Phi0 rows)
-  const bool wide = (jt == 64 && g->I > 32 && g->I <= 256) || (jt == 128 && g->I > 48 && g->I <= 128);
+  // (any I up to the wave-row ceiling: a sample of a few rows still runs 3.6-4x faster padded to
+  // two wave rows than on the fused kernel, whose cost per sample does not fall with I)
+  const bool wide = (jt == 64 && g->I <= 256) || (jt == 128 && g->I <= 128);
   // form: the f32 rank-block body where it fits (R in 5..8: two rank blocks), the bf16-split body
   // for R <= 4 and for the other (I, 64) shapes; TR_DUO_SPLIT=1 takes the split body for R <= 8,
   // =0 the rank-block body only.  (With the non-temporal sample DMA both run at the same rate at
@@ -1095,7 +1097,7 @@ void mnl_duo_geom(MnlGeom* g) {
   const bool rankblock = s32k && g->nrb == 2;
   const bool bsp = (s32k || wide) && g->R <= 8 && !no_split && (force_split || !rankblock);
   if (!bsp && !rankblock) return;
-  const int nw = !bsp ? 4 : jt == 64 ? (g->I + 31) / 32 : 2 * ((g->I + 31) / 32);
+  const int nw = !bsp ? 4 : jt == 64 ? (g->I > 32 ? (g->I + 31) / 32 : 2) : (g->I > 64 ? 2 * ((g->I + 31) / 32) : 4);
   g->du_jt = bsp ? jt : g->J;
   const int wpc = 8 / nw;
   const int64_t spf = (int64_t)(!bsp ? g->I : jt == 64 ? 32 * nw : 16 * nw) * g->du_jt;  // LDS floats per (padded) sample

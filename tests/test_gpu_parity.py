@@ -402,7 +402,10 @@ WIDE_SHAPES = [((300, 64, 64), 10, 8), ((200, 96, 64), 7, 3), ((400, 128, 64), 5
                ((60, 50, 128), 3, 2), ((40, 120, 128), 16, 5),
                # padded row widths: J % 4 == 0 up to the next 64 / 128 (columns past J meet zero Phi1 rows)
                ((200, 128, 48), 10, 8), ((150, 64, 96), 5, 3), ((100, 100, 100), 6, 6), ((120, 200, 40), 4, 8),
-               ((80, 40, 60), 3, 2), ((300, 128, 32), 10, 8), ((200, 64, 28), 4, 3)]
+               ((80, 40, 60), 3, 2), ((300, 128, 32), 10, 8), ((200, 64, 28), 4, 3),
+               # samples of fewer rows than two 32-row waves (64-wide) or four 16-row waves (128-wide)
+               ((300, 16, 64), 10, 8), ((200, 1, 64), 5, 3), ((150, 32, 32), 4, 8), ((400, 8, 128), 6, 5),
+               ((90, 32, 128), 3, 2), ((64, 5, 40), 7, 4), ((100, 48, 128), 4, 8), ((50, 3, 28), 3, 1)]
 
 
 def _split_jt(J):
@@ -410,7 +413,7 @@ def _split_jt(J):
 
 
 def _split_waves(I, J):
-    return (I + 31) // 32 if _split_jt(J) == 64 else 2 * ((I + 31) // 32)
+    return max(2, (I + 31) // 32) if _split_jt(J) == 64 else max(4, 2 * ((I + 31) // 32))
 MNL_SHAPES = [((50, 8, 4), 2, 2), ((200, 16, 8), 10, 4), ((97, 5, 7), 16, 3), ((64, 33), 3, 1),
               ((128, 4, 4, 4), 5, 6), ((333, 32, 32), 10, 8), ((40, 64), 16, 2), ((3, 32), 3, 2),
               # factored single pass: ragged 64-blocks, R % 4 != 0, k ranges split over 2 blocks,
