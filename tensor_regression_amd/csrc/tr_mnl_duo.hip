@@ -24,8 +24,8 @@
 //
 // Envelope (mnl_duo_geom): the rank-block body at (128, 64) / (64, 128) rank 5..8; the bf16-split
 // body at those shapes rank <= 4 and at every (32 NW, 64) sample (NW = 2..8) and (16 NW, 128)
-// sample (NW = 4, 6, 8) rank <= 8, any other I in 33..256 / 49..128 and J % 4 == 0 in 28..128
-// padded to the next of those shapes; <= 16 classes.  Other two-mode shapes run k_mnl_fused
+// sample (NW = 4, 6, 8) rank <= 8, any other I <= 256 / <= 128 and J % 4 == 0 in 28..128
+// padded to the next of those shapes when it fills a third of it; <= 16 classes.  Other two-mode shapes run k_mnl_fused
 // (tr_mnl.hip) where it fits, else the two-pass kernels (DESIGN.md "Multinomial, round 5").
 //
 // Per sample k of a workgroup: wait own LDS-DMA of k -> barrier -> epilogue of k-1 (Z partials
@@ -1101,6 +1101,12 @@ void mnl_duo_geom(MnlGeom* g) {
   g->du_jt = bsp ? jt : g->J;
   const int wpc = 8 / nw;
   const int64_t spf = (int64_t)(!bsp ? g->I : jt == 64 ? 32 * nw : 16 * nw) * g->du_jt;  // LDS floats per (padded) sample
+  // a padded sample fills at least a third of its padded shape (TR_DUO_ANYFILL=1: any fill, for the
+  // tests): below that the two-pass kernels' ~2.6 TB/s on the real bytes beats the body's rate on
+  // the padded ones ((16, 64): 25.8 vs 32.3 % of HBM, (24, 48) at 0.28 even, (24, 64) at 0.375 37.5 vs
+  // 33.1 %; profiles/r05_mnl_fallbacks.txt)
+  const char* anyfill = std::getenv("TR_DUO_ANYFILL");
+  if (bsp && 3 * (int64_t)g->I * g->J < spf && !(anyfill && std::atoi(anyfill) == 1)) return;
   auto carve = [&](int ns) { return duo_carve(g, nw, spf, ns); };
   // the split body at NW = 5, 6 (one workgroup per CU: 80 / 96 KiB in flight with two slots) takes
   // a ring of three samples: (160, 64) 58.9 -> 61.4 %, (192, 64) 65.4 -> 68.5 %, (96, 128) 65.8 ->

@@ -40,7 +40,7 @@ def path(kind):
     f32 rank-block form; the split form is the default only for rank <= 4)."""
     from tensor_regression_amd import standard_tensor_regression as S
     saved = {k: os.environ.get(k) for k in ("TR_FORCE_TWOPASS", "TR_NO_MFMA", "TR_MNL_SPI", "TR_MNL_DUO",
-                                            "TR_DUO_SPLIT")}
+                                            "TR_DUO_SPLIT", "TR_MNL_FUSED_ANY")}
     for k in saved:
         os.environ.pop(k, None)
     if kind == "twopass":
@@ -53,6 +53,9 @@ def path(kind):
         os.environ["TR_MNL_DUO"] = "0"
     if kind == "noduo":
         os.environ["TR_MNL_DUO"] = "0"
+    if kind in ("spi1", "noduo"):
+        # k_mnl_fused on every shape it fits (the plan alone takes it only for samples >= 24 KiB)
+        os.environ["TR_MNL_FUSED_ANY"] = "1"
     if kind == "split":
         os.environ["TR_DUO_SPLIT"] = "1"
     S._plan_cache.clear()
@@ -265,8 +268,12 @@ def test_multinomial_lbfgs_golden(name):
     point the GPU fit ends — near a stationary point, where the gradient is small against its fp32
     summation noise — to within 2x the oracle's own fp32 error against the fp64 closed form; the
     first logged loss to 1e-5; every later logged loss within 1e-5 of
-    the reference's fp32 run OR no further from the fp64 run than the reference's fp32 run is
-    (x2).  Parameters are not compared: they are not identified by this trajectory."""
+    the reference's fp32 run OR no further from the fp64 run than the reference's fp32 run gets
+    anywhere on the trajectory (x2).  The bar is trajectory-wide, not step by step: the reference's
+    own algorithm in fp32 with only the sample order permuted (six seeds, mnllbfgs_basic) ends
+    0.031-0.053 from the fp64 run, with the step of its largest gap moving from seed to seed; the
+    reference's fp32 run itself is 0.036 from it.  Parameters are not compared: they are not
+    identified by this trajectory."""
     from tensor_regression_amd import CP_logistic_regression
     from oracle import cp_oracle
     d = load(name)
@@ -307,7 +314,8 @@ def test_multinomial_lbfgs_golden(name):
                                   m["lbfgs_kwargs"], dtype=torch.float64)
     ours, ref32, ref64 = (np.asarray(v, np.float64) for v in (mm.loss_running, d["loss_running"], r64["loss_running"]))
     assert abs(ours[0] - ref32[0]) <= RTOL * abs(ref32[0])
-    ok = (np.abs(ours - ref32) <= RTOL * np.abs(ref32)) | (np.abs(ours - ref64) <= 2 * np.abs(ref32 - ref64) + RTOL * np.abs(ref64))
+    spread = np.abs(ref32 - ref64).max()
+    ok = (np.abs(ours - ref32) <= RTOL * np.abs(ref32)) | (np.abs(ours - ref64) <= 2 * spread + RTOL * np.abs(ref64))
     assert ok.all(), (ours, ref32, ref64)
     closure_parity(final=True)  # the kernels at the point the GPU trajectory reached
 
@@ -443,15 +451,23 @@ def test_multinomial_sweep_vs_oracle(shape, C, rank, kind):
 def test_multinomial_wide_split_body_selected(shape, C, rank, ring, monkeypatch):
     """(32 NW, 64) and (16 NW, 128) samples with R <= 8 take the split body with NW waves per
     workgroup by default (describe 'form=bf16split waves=NW'), with a ring of three samples at
-    NW = 5, 6 (nbuf=3; TR_DUO_RING=2 keeps two); the results are the sweep's."""
+    NW = 5, 6 (nbuf=3; TR_DUO_RING=2 keeps two); the results are the sweep's.  A padded sample
+    filling less than a third of its padded shape runs the two-pass kernels by default and the
+    split body with TR_DUO_ANYFILL=1."""
     monkeypatch.delenv("TR_DUO_RING", raising=False)
+    monkeypatch.delenv("TR_DUO_ANYFILL", raising=False)
     if ring == "2":
         monkeypatch.setenv("TR_DUO_RING", "2")
-    with path("auto"):
-        desc = _multinomial_sweep(shape, C, rank)
     nw = _split_waves(shape[1], shape[2])
     jt = _split_jt(shape[2])
     padded = shape[1] != (32 if jt == 64 else 16) * nw or shape[2] != jt
+    if 3 * shape[1] * shape[2] < (32 if jt == 64 else 16) * nw * jt:
+        with path("auto"):
+            desc = _multinomial_sweep(shape, C, rank)
+        assert " duo " not in desc and "path=2pass" in desc, desc
+        monkeypatch.setenv("TR_DUO_ANYFILL", "1")
+    with path("auto"):
+        desc = _multinomial_sweep(shape, C, rank)
     # (the padded (16 NW, 128) body with a ring of three spills at NW = 6: the plan takes two slots)
     nbuf = 3 if nw in (5, 6) and ring == "auto" and not (padded and jt == 128) else 2
     assert "form=bf16split" in desc and f"waves={nw} wg/cu={8 // nw} nbuf={nbuf} " in desc, desc

@@ -21,8 +21,9 @@ dev = "cuda:0"
 SHAPES = [((128, 64), 8), ((64, 128), 8), ((128, 64), 3), ((64, 64), 8), ((96, 64), 8), ((160, 64), 8),
           ((192, 64), 8), ((224, 64), 8), ((256, 64), 8), ((64, 64), 3), ((96, 128), 8), ((128, 128), 8),
           ((256, 128), 8)]
-if len(sys.argv) > 1:  # a subset: "I,J" arguments (rank 8)
-    SHAPES = [(tuple(int(v) for v in a.split(",")), 8) for a in sys.argv[1:]]
+if len(sys.argv) > 1:  # a subset: "I,J" or "I,J,R" arguments (rank 8 by default)
+    SHAPES = [((int(a.split(",")[0]), int(a.split(",")[1])), int(a.split(",")[2]) if a.count(",") > 1 else 8)
+              for a in sys.argv[1:]]
 C = 10
 for (I, J), R in SHAPES:
     N = (1 << 29) // (I * J)
