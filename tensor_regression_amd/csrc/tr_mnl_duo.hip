@@ -25,8 +25,9 @@
 // Envelope (mnl_duo_geom): the rank-block body at (128, 64) / (64, 128) rank 5..8; the bf16-split
 // body at those shapes rank <= 4 and at every (32 NW, 64) sample (NW = 2..8) and (16 NW, 128)
 // sample (NW = 4, 6, 8) rank <= 8, any other I <= 256 / <= 128 and J % 4 == 0 in 28..128
-// padded to the next of those shapes when it fills a third of it; <= 16 classes.  Other two-mode shapes run k_mnl_fused
-// (tr_mnl.hip) where it fits, else the two-pass kernels (DESIGN.md "Multinomial, round 5").
+// padded to the next of those shapes when it fills a third of it; <= 16 classes.  Other two-mode
+// shapes run k_mnl_fused (tr_mnl.hip) where it fits and the sample is >= 24 KiB, else the two-pass
+// kernels (DESIGN.md "Multinomial, round 5").
 //
 // Per sample k of a workgroup: wait own LDS-DMA of k -> barrier -> epilogue of k-1 (Z partials
 // of the 2 A-waves, double softmax, Wv, gradient scaling) -> GEMM of k with the DMA of k+1 into
