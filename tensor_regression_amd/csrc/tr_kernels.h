@@ -56,6 +56,12 @@ hipError_t launch_linear_fused(int T, int CH, int grid, const float* X, int64_t 
                                float* gpart, double* dpart, float* yhat, int64_t rows_per_wg,
                                int reverse, const int32_t* stop, hipStream_t st);
 hipError_t prepare_linear_fused(int T, int CH, size_t lds_bytes, int* wg_per_cu);
+// single pass for rows of P <= 128 floats, G = 64 / PQ rows per wave (PQ = linear_packed_pq(P))
+int linear_packed_pq(int64_t P);
+hipError_t launch_linear_packed(int PQ, int grid, const float* X, int64_t N, int64_t P, int64_t xld, const float* B,
+                                const float* bias, const float* y, float scale, float* gpart, double* dpart,
+                                int64_t rows_per_wg, int reverse, const int32_t* stop, hipStream_t st);
+hipError_t prepare_linear_packed(int PQ, int* wg_per_cu);
 // single pass for P beyond one CU's LDS (tr_cluster.hip): clusters of S workgroups, member s
 // owning feature slice [s*slice(CH), (s+1)*slice(CH)), exchanging per-row partial dots
 int linear_cluster_num_ch(void);

@@ -292,6 +292,125 @@ __global__ __launch_bounds__(T) void k_linear_fused(
 }
 
 // ==========================================================================================
+// K2p (linear, single pass, short rows P <= 128): k_linear_fused puts one row on at least one
+// wave (4 T CH >= 256 floats), so a 16-float row leaves 15 of 16 lanes idle and the pass runs at
+// 9 % of HBM.  Here a wave holds G = 64 / PQ rows at once: lane l takes quad q = l % PQ of row
+// l / PQ (PQ = ceil(P / 4) rounded up to a power of two), so one 16-B load per lane covers G
+// consecutive rows (G P floats, contiguous when xld == P).  The dot is a segmented xor-butterfly
+// over the PQ lanes of a row (ds_swizzle, inside a 32-lane half); every lane of the segment
+// gets the same sum, forms r and accumulates r X_n into its own quad of G.  At the end the G
+// segments' quads are summed (xor PQ .. 32), then the 4 waves in LDS in fixed order: the partial
+// slab per workgroup is the one k_linear_fused writes (stride 4 ceil(P / 4), zero past P), so
+// k_reduce_slabs finishes it unchanged.  U blocks of G rows are in flight per wave.
+//   Row range per workgroup as k_linear_fused (rows_per_wg, reverse: blocks taken backwards);
+//   a block's buffer descriptor starts at its first row and ends at the last row's float P, so
+//   rows past the range and floats past P of the last row read zero; floats past P of the other
+//   rows (the next row's data) are zeroed in registers.
+// ==========================================================================================
+template <int PQ, int U>
+__global__ __launch_bounds__(256) void k_linear_packed(
+    const float* __restrict__ X, int64_t N, int64_t P, int64_t xld, const float* __restrict__ B,
+    const float* __restrict__ bias_p, const float* __restrict__ y, float scale,
+    float* __restrict__ gpart, double* __restrict__ dpart, int64_t rows_per_wg, int reverse,
+    const int32_t* __restrict__ stop) {
+  constexpr int G = TR_WAVE / PQ;  // rows per block
+  constexpr int NW = 4;
+  static_assert(PQ >= 1 && PQ <= 32 && (PQ & (PQ - 1)) == 0, "PQ: a power of two <= 32");
+  __shared__ float4 sg[NW][PQ];
+  __shared__ double sd[NW][2];
+  if (stop != nullptr && *stop != 0) return;
+  const int t = threadIdx.x;
+  const int lane = t & (TR_WAVE - 1);
+  const int wv = t / TR_WAVE;
+  const int q = lane % PQ;
+  const int seg = lane / PQ;
+  const int64_t Pq = (P + 3) / 4;
+  // this lane's B quad and the mask of its floats below P
+  const int e0 = 4 * q;
+  const bool m0 = e0 < P, m1 = e0 + 1 < P, m2 = e0 + 2 < P, m3 = e0 + 3 < P;
+  float4 b = make_float4(m0 ? B[e0] : 0.f, m1 ? B[e0 + 1] : 0.f, m2 ? B[e0 + 2] : 0.f, m3 ? B[e0 + 3] : 0.f);
+  const float bias = bias_p != nullptr ? *bias_p : 0.f;
+
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_wg;
+  const int64_t r1 = r0 + rows_per_wg < N ? r0 + rows_per_wg : N;
+  const int64_t nr = r1 > r0 ? r1 - r0 : 0;
+  const int64_t nb = (nr + G - 1) / G;
+  const int voff = (int)((int64_t)seg * xld * 4 + 16 * q);
+  const char* Xb = reinterpret_cast<const char*>(X);
+
+  float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+  double sse = 0.0, rsum = 0.0;
+#pragma unroll 1
+  for (int64_t k0 = (int64_t)wv * U; k0 < nb; k0 += (int64_t)NW * U) {
+    float4 x[U];
+    int64_t fr[U];
+    int rin[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t k = k0 + u;
+      const int64_t kb = reverse ? nb - 1 - k : k;
+      fr[u] = r0 + kb * G;
+      const int64_t left = r1 - fr[u];
+      rin[u] = k < nb ? (int)(left < G ? left : G) : 0;
+      const int nrec = rin[u] > 0 ? (int)((int64_t)(rin[u] - 1) * xld * 4 + P * 4) : 0;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<char*>(Xb + (k < nb ? fr[u] : 0) * xld * 4), (short)0, nrec, 0x00020000);
+      const tr_f4 v = __builtin_bit_cast(tr_f4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, TR_X_AUX));
+      x[u] = make_float4(m0 ? v.x : 0.f, m1 ? v.y : 0.f, m2 ? v.z : 0.f, m3 ? v.w : 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float s = tr_dot4(x[u], b, 0.f);
+      if (PQ >= 32) s += tr_swz_xor<0x401F>(s);
+      if (PQ >= 16) s += tr_swz_xor<0x201F>(s);
+      if (PQ >= 8) s += tr_swz_xor<0x101F>(s);
+      if (PQ >= 4) s += tr_swz_xor<0x081F>(s);
+      if (PQ >= 2) s += tr_swz_xor<0x041F>(s);
+      const bool valid = seg < rin[u];
+      const float e = valid ? s + bias - y[fr[u] + seg] : 0.f;
+      const float r = e * scale;
+      tr_axpy4(r, x[u], g);
+      if (q == 0) {
+        sse += (double)e * (double)e;
+        rsum += (double)r;
+      }
+    }
+  }
+  // the G segments' quads, then the waves in fixed order
+#pragma unroll
+  for (int o = PQ; o < TR_WAVE; o <<= 1) {
+    g.x += __shfl_xor(g.x, o, TR_WAVE);
+    g.y += __shfl_xor(g.y, o, TR_WAVE);
+    g.z += __shfl_xor(g.z, o, TR_WAVE);
+    g.w += __shfl_xor(g.w, o, TR_WAVE);
+  }
+  sse = tr_wave_allreduce_d(sse);
+  rsum = tr_wave_allreduce_d(rsum);
+  if (seg == 0) sg[wv][q] = g;
+  if (lane == 0) {
+    sd[wv][0] = sse;
+    sd[wv][1] = rsum;
+  }
+  __syncthreads();
+  if (t < PQ && t < Pq) {
+    float4 a = sg[0][t];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) {
+      const float4 c = sg[w][t];
+      a.x += c.x;
+      a.y += c.y;
+      a.z += c.z;
+      a.w += c.w;
+    }
+    reinterpret_cast<float4*>(gpart + (int64_t)blockIdx.x * (4 * Pq))[t] = a;
+  }
+  if (t == 0) {
+    dpart[2 * blockIdx.x + 0] = sd[0][0] + sd[1][0] + sd[2][0] + sd[3][0];
+    dpart[2 * blockIdx.x + 1] = sd[0][1] + sd[1][1] + sd[2][1] + sd[3][1];
+  }
+}
+
+// ==========================================================================================
 // K2' two-pass forward: Z[n, c] = <X_n, Bt_c>  (+ fused epilogue per MODE)
 //   MODE_LIN_TRAIN : r[n] = (z + bias - y) * scale; per-wave (sse, sum r)
 //   MODE_LIN_PRED  : out[n] = z + bias
@@ -1178,6 +1297,66 @@ hipError_t prepare_linear_fused(int T, int CH, size_t lds_bytes, int* wg_per_cu)
   if (attr.localSizeBytes > 0) return hipSuccess;  // spills: reject
   int nb = 0;
   err = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, e->kernel, T, lds_bytes);
+  if (err != hipSuccess) return err;
+  *wg_per_cu = nb;
+  return hipSuccess;
+}
+
+// ---- single pass, short rows ---------------------------------------------------------------
+#ifndef TR_PACKED_U
+#define TR_PACKED_U 4
+#endif
+template <int PQ>
+static hipError_t packed_launch_t(int grid, const float* X, int64_t N, int64_t P, int64_t xld, const float* B,
+                                  const float* bias, const float* y, float scale, float* gpart, double* dpart,
+                                  int64_t rpw, int reverse, const int32_t* stop, hipStream_t st) {
+  if (P < 1 || P > 4 * PQ) return hipErrorInvalidValue;
+  if ((int64_t)(TR_WAVE / PQ) * xld * 4 + P * 4 > INT32_MAX) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((k_linear_packed<PQ, TR_PACKED_U>), dim3(grid), dim3(256), 0, st, X, N, P, xld, B, bias, y,
+                     scale, gpart, dpart, rpw, reverse, stop);
+  return hipGetLastError();
+}
+static const void* packed_kernel(int PQ) {
+  switch (PQ) {
+    case 1: return reinterpret_cast<const void*>(&k_linear_packed<1, TR_PACKED_U>);
+    case 2: return reinterpret_cast<const void*>(&k_linear_packed<2, TR_PACKED_U>);
+    case 4: return reinterpret_cast<const void*>(&k_linear_packed<4, TR_PACKED_U>);
+    case 8: return reinterpret_cast<const void*>(&k_linear_packed<8, TR_PACKED_U>);
+    case 16: return reinterpret_cast<const void*>(&k_linear_packed<16, TR_PACKED_U>);
+    case 32: return reinterpret_cast<const void*>(&k_linear_packed<32, TR_PACKED_U>);
+  }
+  return nullptr;
+}
+int linear_packed_pq(int64_t P) {
+  if (P < 1 || P > 128) return 0;
+  int pq = 1;
+  while (4 * pq < P) pq *= 2;
+  return pq;
+}
+hipError_t launch_linear_packed(int PQ, int grid, const float* X, int64_t N, int64_t P, int64_t xld, const float* B,
+                                const float* bias, const float* y, float scale, float* gpart, double* dpart,
+                                int64_t rows_per_wg, int reverse, const int32_t* stop, hipStream_t st) {
+  switch (PQ) {
+    case 1: return packed_launch_t<1>(grid, X, N, P, xld, B, bias, y, scale, gpart, dpart, rows_per_wg, reverse, stop, st);
+    case 2: return packed_launch_t<2>(grid, X, N, P, xld, B, bias, y, scale, gpart, dpart, rows_per_wg, reverse, stop, st);
+    case 4: return packed_launch_t<4>(grid, X, N, P, xld, B, bias, y, scale, gpart, dpart, rows_per_wg, reverse, stop, st);
+    case 8: return packed_launch_t<8>(grid, X, N, P, xld, B, bias, y, scale, gpart, dpart, rows_per_wg, reverse, stop, st);
+    case 16: return packed_launch_t<16>(grid, X, N, P, xld, B, bias, y, scale, gpart, dpart, rows_per_wg, reverse, stop, st);
+    case 32: return packed_launch_t<32>(grid, X, N, P, xld, B, bias, y, scale, gpart, dpart, rows_per_wg, reverse, stop, st);
+  }
+  return hipErrorInvalidValue;
+}
+// spill-free occupancy of the short-row pass (workgroups of 256 per CU; 0 = unusable)
+hipError_t prepare_linear_packed(int PQ, int* wg_per_cu) {
+  *wg_per_cu = 0;
+  const void* k = packed_kernel(PQ);
+  if (k == nullptr) return hipErrorInvalidValue;
+  hipFuncAttributes attr;
+  hipError_t err = hipFuncGetAttributes(&attr, k);
+  if (err != hipSuccess) return err;
+  if (attr.localSizeBytes > 0) return hipSuccess;
+  int nb = 0;
+  err = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 256, 0);
   if (err != hipSuccess) return err;
   *wg_per_cu = nb;
   return hipSuccess;

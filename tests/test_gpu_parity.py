@@ -40,7 +40,7 @@ def path(kind):
     f32 rank-block form; the split form is the default only for rank <= 4)."""
     from tensor_regression_amd import standard_tensor_regression as S
     saved = {k: os.environ.get(k) for k in ("TR_FORCE_TWOPASS", "TR_NO_MFMA", "TR_MNL_SPI", "TR_MNL_DUO",
-                                            "TR_DUO_SPLIT", "TR_MNL_FUSED_ANY")}
+                                            "TR_DUO_SPLIT", "TR_MNL_FUSED_ANY", "TR_NO_PACKED")}
     for k in saved:
         os.environ.pop(k, None)
     if kind == "twopass":
@@ -58,6 +58,8 @@ def path(kind):
         os.environ["TR_MNL_FUSED_ANY"] = "1"
     if kind == "split":
         os.environ["TR_DUO_SPLIT"] = "1"
+    if kind == "nopacked":  # linear rows of P <= 128 on k_linear_fused instead of k_linear_packed
+        os.environ["TR_NO_PACKED"] = "1"
     S._plan_cache.clear()
     try:
         yield
@@ -344,6 +346,16 @@ LIN_SHAPES = [
     ((200, 100, 100), 4),      # P = 10000 -> T = 512, CH = 5 (2.4 % padding)
     ((150, 160, 160), 8),      # P = 25600 -> T = 1024, CH = 7
     ((90, 250, 130), 3),       # P = 32500 -> T = 1024, CH = 8 (0.8 %)
+    # short rows (P <= 128): k_linear_packed, 64 / PQ rows per wave, the last block ragged
+    ((5000, 2, 2), 3),         # P = 4: PQ = 1, 64 rows per wave
+    ((3001, 3, 3), 2),         # P = 9: PQ = 4, one quad partial, one past P
+    ((129, 1, 6), 2),          # P = 6: PQ = 2
+    ((64, 7), 2),              # one feature mode, P = 7
+    ((4097, 4, 8), 8),         # P = 32: PQ = 8
+    ((1000, 8, 8), 4),         # P = 64: PQ = 16
+    ((777, 12, 10), 5),        # P = 120: PQ = 32, 2 rows per wave
+    ((999, 5, 5, 5), 3),       # P = 125
+    ((3, 4, 4), 2),            # fewer rows than one block
 ]
 PADDED_FUSED = [((200, 100, 100), 4), ((150, 160, 160), 8), ((90, 250, 130), 3), ((129, 100, 101), 2),
                 ((7, 5, 3), 1), ((257, 6, 7, 8, 3), 5)]
@@ -360,14 +372,21 @@ def test_linear_padded_rows_take_the_fused_pass(shape, rank):
         model = CP_linear_regression(X.shape, rank=rank, device=DEV)
         plan = model._get_plan(X, shape[0])
         P = int(np.prod(shape[1:]))
+        assert "path=fused-1pass" in plan.describe, plan.describe
+        if P <= 128:  # short rows: the packed pass, PQ the power of two >= P / 4
+            pq = int(plan.describe.split(" pk=")[1].split()[0])
+            assert 4 * pq >= P and (pq == 1 or 2 * pq < P), plan.describe
+            return
         T = int(plan.describe.split(" T=")[1].split()[0])
         CH = int(plan.describe.split(" CH=")[1].split()[0])
-        assert "path=fused-1pass" in plan.describe and P <= 4 * T * CH <= max(1.25 * P, 4 * 64), plan.describe
+        assert P <= 4 * T * CH <= max(1.25 * P, 4 * 64), plan.describe
 
 
-@pytest.mark.parametrize("kind", ["auto", "twopass"])
+@pytest.mark.parametrize("kind", ["auto", "twopass", "nopacked"])
 @pytest.mark.parametrize("shape,rank", LIN_SHAPES)
 def test_linear_sweep_vs_oracle(shape, rank, kind):
+    if kind == "nopacked" and int(np.prod(shape[1:])) > 128:
+        pytest.skip("rows above 128 floats never take the packed pass")
     from oracle import cp_oracle
     from tensor_regression_amd import CP_linear_regression
     g = torch.Generator().manual_seed(hash((shape, rank)) % 2**31)
@@ -396,6 +415,41 @@ def test_linear_sweep_vs_oracle(shape, rank, kind):
         yh = plan.forward(Xd, arena, model.weights)
         np.testing.assert_allclose(yh.cpu().numpy(), ref["y_hat"].reshape(-1), rtol=RTOL,
                                    atol=RTOL * np.abs(ref["y_hat"]).max())
+
+
+@pytest.mark.parametrize("pad", [5, -3])
+@pytest.mark.parametrize("shape", [(700, 4, 5), (300, 3, 3), (2000, 2, 2)])
+def test_linear_packed_strided_rows(shape, pad):
+    """k_linear_packed on a view whose rows are P + pad floats apart (pad < 0: overlapping windows):
+    the block descriptor ends at the last row's float P and the floats past P of the other rows (the
+    next row's data) are zeroed in registers; same numbers as the contiguous copy through the oracle."""
+    from oracle import cp_oracle
+    from tensor_regression_amd import CP_linear_regression
+    N, P = shape[0], int(np.prod(shape[1:]))
+    g = torch.Generator().manual_seed(7 + P + pad)
+    base = torch.randn(N * (P + pad) + P, generator=g)
+    Xv = torch.as_strided(base, (N,) + shape[1:], (P + pad,) + tuple(torch.empty(shape[1:]).stride()))
+    X = Xv.contiguous()
+    y = torch.randn(N, generator=g)
+    Bcp0 = [torch.randn(d, 3, generator=g) * 0.3 for d in shape[1:]]
+    w = torch.rand(3, generator=g) + 0.5
+    ref = cp_oracle.linear_loss_grad(X, y, Bcp0, torch.tensor([0.25]), w, [False] * (len(shape) - 1), 0.01)
+    with path("auto"):
+        model = CP_linear_regression(X.shape, rank=3, weights=w.numpy(), device=DEV,
+                                     Bcp_init=[b.to(DEV) for b in Bcp0], bias_init=0.25)
+        bd = base.to(DEV)
+        Xd = torch.as_strided(bd, Xv.shape, Xv.stride())
+        yd = y.to(DEV)
+        plan = model._get_plan(Xd, N)
+        arena = plan.pack(model.Bcp, model.bias)
+        grad = torch.zeros(plan.num_grads, device=DEV)
+        gtot = torch.zeros(plan.num_params, device=DEV)
+        loss = torch.zeros(1, device=DEV)
+        plan.loss_grad(Xd, yd, None, float(N), arena, model.weights, grad)
+        plan.finalize_grad(arena, grad, 0.01, gtot, loss)
+        assert " pk=" in plan.describe, plan.describe
+        assert abs(loss.item() - ref["loss"]) <= RTOL * abs(ref["loss"])
+        _assert_factors(plan.factor_views(gtot), ref["grads"])
 
 
 # (shape, C, rank) of the split body's (32 NW, 64) and (16 NW, 128) sample shapes: one per wave
