@@ -1303,27 +1303,46 @@ hipError_t prepare_linear_fused(int T, int CH, size_t lds_bytes, int* wg_per_cu)
 }
 
 // ---- single pass, short rows ---------------------------------------------------------------
-#ifndef TR_PACKED_U
-#define TR_PACKED_U 4
-#endif
+// U blocks in flight per wave: 4, or 2 / 8 with TR_PACKED_U (measurement knob)
+static int packed_u() {
+  static const int u = [] {
+    const char* e = std::getenv("TR_PACKED_U");
+    const int v = e != nullptr ? std::atoi(e) : 4;
+    return v == 8 || v == 2 ? v : 4;
+  }();
+  return u;
+}
 template <int PQ>
 static hipError_t packed_launch_t(int grid, const float* X, int64_t N, int64_t P, int64_t xld, const float* B,
                                   const float* bias, const float* y, float scale, float* gpart, double* dpart,
                                   int64_t rpw, int reverse, const int32_t* stop, hipStream_t st) {
   if (P < 1 || P > 4 * PQ) return hipErrorInvalidValue;
   if ((int64_t)(TR_WAVE / PQ) * xld * 4 + P * 4 > INT32_MAX) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((k_linear_packed<PQ, TR_PACKED_U>), dim3(grid), dim3(256), 0, st, X, N, P, xld, B, bias, y,
-                     scale, gpart, dpart, rpw, reverse, stop);
+  if (packed_u() == 8)
+    hipLaunchKernelGGL((k_linear_packed<PQ, 8>), dim3(grid), dim3(256), 0, st, X, N, P, xld, B, bias, y, scale,
+                       gpart, dpart, rpw, reverse, stop);
+  else if (packed_u() == 2)
+    hipLaunchKernelGGL((k_linear_packed<PQ, 2>), dim3(grid), dim3(256), 0, st, X, N, P, xld, B, bias, y, scale,
+                       gpart, dpart, rpw, reverse, stop);
+  else
+    hipLaunchKernelGGL((k_linear_packed<PQ, 4>), dim3(grid), dim3(256), 0, st, X, N, P, xld, B, bias, y, scale,
+                       gpart, dpart, rpw, reverse, stop);
   return hipGetLastError();
+}
+template <int PQ>
+static const void* packed_kernel_t() {
+  return packed_u() == 8   ? reinterpret_cast<const void*>(&k_linear_packed<PQ, 8>)
+         : packed_u() == 2 ? reinterpret_cast<const void*>(&k_linear_packed<PQ, 2>)
+                           : reinterpret_cast<const void*>(&k_linear_packed<PQ, 4>);
 }
 static const void* packed_kernel(int PQ) {
   switch (PQ) {
-    case 1: return reinterpret_cast<const void*>(&k_linear_packed<1, TR_PACKED_U>);
-    case 2: return reinterpret_cast<const void*>(&k_linear_packed<2, TR_PACKED_U>);
-    case 4: return reinterpret_cast<const void*>(&k_linear_packed<4, TR_PACKED_U>);
-    case 8: return reinterpret_cast<const void*>(&k_linear_packed<8, TR_PACKED_U>);
-    case 16: return reinterpret_cast<const void*>(&k_linear_packed<16, TR_PACKED_U>);
-    case 32: return reinterpret_cast<const void*>(&k_linear_packed<32, TR_PACKED_U>);
+    case 1: return packed_kernel_t<1>();
+    case 2: return packed_kernel_t<2>();
+    case 4: return packed_kernel_t<4>();
+    case 8: return packed_kernel_t<8>();
+    case 16: return packed_kernel_t<16>();
+    case 32: return packed_kernel_t<32>();
   }
   return nullptr;
 }
