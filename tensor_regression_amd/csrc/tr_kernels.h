@@ -82,7 +82,7 @@ hipError_t launch_rows(int C, int mode, int W, const float* X, int64_t N, int64_
                        hipStream_t st);
 int64_t rows_num_waves(int C, int64_t N);
 bool rows_mfma_supported(int C, int64_t P);
-int64_t rows_mfma_num_waves(int64_t N);
+int64_t rows_mfma_num_waves(int64_t N, int64_t P);
 hipError_t launch_rows_mfma(int mode, const float* X, int64_t N, int64_t P, int64_t xld, const float* Bt, int C,
                             const int64_t* lab, const float* class_w, float scale, float* out, double* dpart,
                             const int32_t* stop, hipStream_t st);

@@ -1434,23 +1434,44 @@ hipError_t launch_rows(int C, int mode, int W, const float* X, int64_t N, int64_
 }
 
 // ---- multinomial forward on MFMA ------------------------------------------------------------
-static const int kMfmaRT = 2;
+// row tiles of 16 per wave by row width (TR_MFMA_RT = 1 / 2 / 4 overrides): one for rows of
+// <= 256 floats (more waves for short rows: (16, 16) 0.690 -> 0.590 ms), four from 4096 ((64, 64)
+// 0.454 -> 0.394 ms, (128, 64) 0.376 -> 0.366 ms), else two (profiles/r05_mnl_rows_rt.txt)
+static int mfma_rt(int64_t P) {
+  static const int forced = [] {
+    const char* e = std::getenv("TR_MFMA_RT");
+    const int v = e != nullptr ? std::atoi(e) : 0;
+    return v == 1 || v == 2 || v == 4 ? v : 0;
+  }();
+  if (forced) return forced;
+  return P <= 256 ? 1 : (P >= 4096 ? 4 : 2);
+}
 bool rows_mfma_supported(int C, int64_t P) { return C >= 1 && C <= 16 && P % 32 == 0; }
-int64_t rows_mfma_num_waves(int64_t N) { return (N + 16 * kMfmaRT - 1) / (16 * kMfmaRT); }
+int64_t rows_mfma_num_waves(int64_t N, int64_t P) { return (N + 16 * mfma_rt(P) - 1) / (16 * mfma_rt(P)); }
+template <int RT>
+static void rows_mfma_go(int mode, unsigned grid, const float* X, int64_t N, int64_t P, int64_t xld, const float* Bt,
+                         int C, const int64_t* lab, const float* class_w, float scale, float* out, double* dpart,
+                         const int32_t* stop, hipStream_t st) {
+  if (mode == MODE_MNL_TRAIN)
+    hipLaunchKernelGGL((k_rows_mfma<MODE_MNL_TRAIN, RT>), dim3(grid), dim3(256), 0, st, X, N, P, xld, Bt, C, lab,
+                       class_w, scale, out, dpart, stop, (int64_t)C);
+  else
+    hipLaunchKernelGGL((k_rows_mfma<MODE_MNL_PRED, RT>), dim3(grid), dim3(256), 0, st, X, N, P, xld, Bt, C, lab,
+                       class_w, scale, out, dpart, stop, (int64_t)C);
+}
 
 hipError_t launch_rows_mfma(int mode, const float* X, int64_t N, int64_t P, int64_t xld, const float* Bt, int C,
                             const int64_t* lab, const float* class_w, float scale, float* out, double* dpart,
                             const int32_t* stop, hipStream_t st) {
-  const int64_t waves = rows_mfma_num_waves(N);
+  const int64_t waves = rows_mfma_num_waves(N, P);
   const unsigned grid = cdiv(waves, 4);
-  if (mode == MODE_MNL_TRAIN)
-    hipLaunchKernelGGL((k_rows_mfma<MODE_MNL_TRAIN, kMfmaRT>), dim3(grid), dim3(256), 0, st, X, N, P, xld, Bt, C, lab,
-                       class_w, scale, out, dpart, stop, (int64_t)C);
-  else if (mode == MODE_MNL_PRED)
-    hipLaunchKernelGGL((k_rows_mfma<MODE_MNL_PRED, kMfmaRT>), dim3(grid), dim3(256), 0, st, X, N, P, xld, Bt, C, lab,
-                       class_w, scale, out, dpart, stop, (int64_t)C);
+  if (mode != MODE_MNL_TRAIN && mode != MODE_MNL_PRED) return hipErrorInvalidValue;
+  if (mfma_rt(P) == 1)
+    rows_mfma_go<1>(mode, grid, X, N, P, xld, Bt, C, lab, class_w, scale, out, dpart, stop, st);
+  else if (mfma_rt(P) == 4)
+    rows_mfma_go<4>(mode, grid, X, N, P, xld, Bt, C, lab, class_w, scale, out, dpart, stop, st);
   else
-    return hipErrorInvalidValue;
+    rows_mfma_go<2>(mode, grid, X, N, P, xld, Bt, C, lab, class_w, scale, out, dpart, stop, st);
   return hipGetLastError();
 }
 
@@ -1493,8 +1514,8 @@ hipError_t launch_mnl_logits(int C, int mfma, int W, const float* X, int64_t N, 
   const int ntiles = (C + 15) / 16;
   if (mfma) {  // every class tile in one launch (grid.y); Bt padded to 16 * ntiles class rows
     if (P % 32 != 0) return hipErrorInvalidValue;
-    const int64_t waves = rows_mfma_num_waves(N);
-    hipLaunchKernelGGL((k_rows_mfma<MODE_MNL_LOGITS, kMfmaRT>), dim3(cdiv(waves, 4), (unsigned)ntiles), dim3(256), 0,
+    const int64_t waves = (N + 31) / 32;  // two row tiles per wave
+    hipLaunchKernelGGL((k_rows_mfma<MODE_MNL_LOGITS, 2>), dim3(cdiv(waves, 4), (unsigned)ntiles), dim3(256), 0,
                        st, X, N, P, xld, Bt, C, nullptr, nullptr, 0.f, Z, nullptr, stop, (int64_t)C);
     return hipGetLastError();
   }
