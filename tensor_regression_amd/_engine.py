@@ -529,6 +529,49 @@ def agree(process_group, fn):
     return out
 
 
+def fit_start(process_group, fn, norm_of, size_of):
+    """The start of a sharded fit in ONE collective: run this rank's preparation `fn()` (as
+    `agree` does), then a single MAX all-reduce of a float64 vector settles
+      - whether `fn` raised on any rank (every rank raises then, like `agree`);
+      - that every rank's parameter arena has the same size, `size_of(out)` (ValueError on every
+        rank otherwise, like `check_uniform`: no rank is left in a later collective);
+      - the global normaliser, the sum of every rank's `norm_of(out)` (the sample count, or the
+        class-weight total of the CE mean): each rank writes its value into its own slot, -inf
+        into the others, so the MAX hands every rank every value, summed in rank order.
+    One host read of the result.  Replaces agree + an all-reduce of the normaliser + the arena
+    check of sync_replicas (three collectives and three host synchronisations per fit call: at
+    world 1 on RCCL most of the process-group path's per-call cost, tools/pg_account.py).
+    Returns (fn's result, global normaliser)."""
+    import torch.distributed as dist
+    world = dist.get_world_size(process_group)
+    me = dist.get_rank(process_group)
+    err, out = None, None
+    try:
+        out = fn()
+    except Exception as e:  # re-raised below, after the other ranks have been told
+        err = e
+    v = torch.full((3 + world,), float("-inf"), dtype=torch.float64)
+    v[0] = 0.0 if err is None else 1.0
+    if err is None:
+        size = float(size_of(out))
+        v[1], v[2], v[3 + me] = size, -size, float(norm_of(out))
+    v = v.to(collective_device(process_group))
+    dist.all_reduce(v, op=dist.ReduceOp.MAX, group=process_group)
+    r = v.tolist()
+    if err is not None:
+        raise err
+    if r[0] > 0:
+        raise RuntimeError("the sharded fit failed on another rank of the process group (see that rank's error); "
+                           "no rank started fitting")
+    if r[1] != size or -r[2] != size:
+        raise ValueError(f"ranks disagree on the parameter arena size (this rank {int(size)}, max {int(r[1])}, "
+                         f"min {int(-r[2])}); every rank's model must have the same factor shapes")
+    total = 0.0
+    for x in r[3:]:
+        total += x
+    return out, total
+
+
 def check_uniform(value, process_group, what, device):
     """Raise ValueError on EVERY rank when the ranks disagree on an integer (one all-reduce), so a
     mismatch cannot leave some ranks blocked in a later collective."""
@@ -540,7 +583,7 @@ def check_uniform(value, process_group, what, device):
                          "every rank's model must have the same factor shapes")
 
 
-def sync_replicas(arena, process_group):
+def sync_replicas(arena, process_group, checked=False):
     """Start every rank's replica from the same parameters (multi-GPU fit_Adam).
 
     The ranks must agree on the arena layout (a multinomial model takes the global class set
@@ -548,9 +591,11 @@ def sync_replicas(arena, process_group):
     all-reduce so a mismatch raises on every rank instead of hanging in the per-iteration
     all-reduce — and then
     take group rank 0's parameters (one broadcast per fit).  From there the replicas stay in
-    lock-step: every rank applies the identical step to the bitwise-identical all-reduced sums."""
+    lock-step: every rank applies the identical step to the bitwise-identical all-reduced sums.
+    checked: the arena sizes were already compared (fit_start)."""
     import torch.distributed as dist
-    check_uniform(arena.numel(), process_group, "the parameter arena size", arena.device)
+    if not checked:
+        check_uniform(arena.numel(), process_group, "the parameter arena size", arena.device)
     src = dist.get_global_rank(process_group, 0) if process_group is not None else 0
     dist.broadcast(arena, src=src, group=process_group)
 
@@ -801,7 +846,7 @@ def gradient_allreduce(process_group, device_index):
 
 
 def run_adam_fit(plan, X, target, class_weight, norm, arena, weights, lambda_L2, max_iter, tol, patience,
-                 hp, loss_running, verbose_cb=None, process_group=None, sync_every=64):
+                 hp, loss_running, verbose_cb=None, process_group=None, sync_every=64, arena_checked=False):
     """The fit_Adam loop (standard…py:453-470 / multinomial…py:447-465), device resident.
 
     Returns (convergence_reached, number_of_iterations_run).  `loss_running` is extended in place
@@ -814,7 +859,7 @@ def run_adam_fit(plan, X, target, class_weight, norm, arena, weights, lambda_L2,
     fdt = getattr(plan, "dtype", torch.float32)
     allreduce = None
     if process_group is not None:
-        sync_replicas(arena, process_group)
+        sync_replicas(arena, process_group, checked=arena_checked)
         allreduce = gradient_allreduce(process_group, getattr(plan, "dev", None))
     grad, m, v, vmax, stop, tmp = fit_state(plan, fdt, hp["amsgrad"])
     base = len(loss_running)

@@ -25,31 +25,16 @@
 namespace tr {
 
 // ------------------------------------------------------------------------------------------
-// X stream load policy.  Plain loads keep the most recently streamed rows in the 256 MiB
-// Infinity Cache, which the alternating traversal direction (see launch code) re-uses.
+// X stream load policy: X is read once per pass (>> the 256 MiB Infinity Cache), so its loads
+// are non-temporal: 6.80 vs 6.32 TB/s with the default policy on the single-pass kernel, 6.82 vs
+// 6.06 TB/s on a grid-stride read probe (tools/hbm_probe.hip).
 // ------------------------------------------------------------------------------------------
-// X is read once per pass (>> the 256 MiB Infinity Cache): non-temporal loads measured
-// 6.80 vs 6.32 TB/s on the single-pass kernel and 6.82 vs 6.06 TB/s on a grid-stride read probe
-// (tools/hbm_probe.hip).  TR_X_NT=0 builds the default-policy variant for comparison.
-#ifndef TR_X_NT
-#define TR_X_NT 1
-#endif
-#define TR_X_AUX (TR_X_NT ? 2 : 0)  // buffer-load cache-policy bits (2 = nt)
+#define TR_X_AUX 2  // buffer-load cache-policy bits (2 = nt)
 __device__ __forceinline__ float4 ldx(const float4* p) {
-#if TR_X_NT
   const tr_f4 v = __builtin_nontemporal_load(reinterpret_cast<const tr_f4*>(p));
   return make_float4(v.x, v.y, v.z, v.w);
-#else
-  return *p;
-#endif
 }
-__device__ __forceinline__ float ldx(const float* p) {
-#if TR_X_NT
-  return __builtin_nontemporal_load(p);
-#else
-  return *p;
-#endif
-}
+__device__ __forceinline__ float ldx(const float* p) { return __builtin_nontemporal_load(p); }
 
 // ==========================================================================================
 // K1a: factor preparation  (non_neg_fn, standard…py:53-85; multinomial…py:116-146)
@@ -1303,37 +1288,20 @@ hipError_t prepare_linear_fused(int T, int CH, size_t lds_bytes, int* wg_per_cu)
 }
 
 // ---- single pass, short rows ---------------------------------------------------------------
-// U blocks in flight per wave: 4, or 2 / 8 with TR_PACKED_U (measurement knob)
-static int packed_u() {
-  static const int u = [] {
-    const char* e = std::getenv("TR_PACKED_U");
-    const int v = e != nullptr ? std::atoi(e) : 4;
-    return v == 8 || v == 2 ? v : 4;
-  }();
-  return u;
-}
+// U = 4 blocks in flight per wave (2: 0-10 points lower, 8: 4-11 lower; DESIGN.md k_linear_packed)
 template <int PQ>
 static hipError_t packed_launch_t(int grid, const float* X, int64_t N, int64_t P, int64_t xld, const float* B,
                                   const float* bias, const float* y, float scale, float* gpart, double* dpart,
                                   int64_t rpw, int reverse, const int32_t* stop, hipStream_t st) {
   if (P < 1 || P > 4 * PQ) return hipErrorInvalidValue;
   if ((int64_t)(TR_WAVE / PQ) * xld * 4 + P * 4 > INT32_MAX) return hipErrorInvalidValue;
-  if (packed_u() == 8)
-    hipLaunchKernelGGL((k_linear_packed<PQ, 8>), dim3(grid), dim3(256), 0, st, X, N, P, xld, B, bias, y, scale,
-                       gpart, dpart, rpw, reverse, stop);
-  else if (packed_u() == 2)
-    hipLaunchKernelGGL((k_linear_packed<PQ, 2>), dim3(grid), dim3(256), 0, st, X, N, P, xld, B, bias, y, scale,
-                       gpart, dpart, rpw, reverse, stop);
-  else
-    hipLaunchKernelGGL((k_linear_packed<PQ, 4>), dim3(grid), dim3(256), 0, st, X, N, P, xld, B, bias, y, scale,
-                       gpart, dpart, rpw, reverse, stop);
+  hipLaunchKernelGGL((k_linear_packed<PQ, 4>), dim3(grid), dim3(256), 0, st, X, N, P, xld, B, bias, y, scale, gpart,
+                     dpart, rpw, reverse, stop);
   return hipGetLastError();
 }
 template <int PQ>
 static const void* packed_kernel_t() {
-  return packed_u() == 8   ? reinterpret_cast<const void*>(&k_linear_packed<PQ, 8>)
-         : packed_u() == 2 ? reinterpret_cast<const void*>(&k_linear_packed<PQ, 2>)
-                           : reinterpret_cast<const void*>(&k_linear_packed<PQ, 4>);
+  return reinterpret_cast<const void*>(&k_linear_packed<PQ, 4>);
 }
 static const void* packed_kernel(int PQ) {
   switch (PQ) {
@@ -1434,16 +1402,10 @@ hipError_t launch_rows(int C, int mode, int W, const float* X, int64_t N, int64_
 }
 
 // ---- multinomial forward on MFMA ------------------------------------------------------------
-// row tiles of 16 per wave by row width (TR_MFMA_RT = 1 / 2 / 4 overrides): one for rows of
+// row tiles of 16 per wave by row width: one for rows of
 // <= 256 floats (more waves for short rows: (16, 16) 0.690 -> 0.590 ms), four from 4096 ((64, 64)
 // 0.454 -> 0.394 ms, (128, 64) 0.376 -> 0.366 ms), else two (profiles/r05_mnl_rows_rt.txt)
 static int mfma_rt(int64_t P) {
-  static const int forced = [] {
-    const char* e = std::getenv("TR_MFMA_RT");
-    const int v = e != nullptr ? std::atoi(e) : 0;
-    return v == 1 || v == 2 || v == 4 ? v : 0;
-  }();
-  if (forced) return forced;
   return P <= 256 ? 1 : (P >= 4096 ? 4 : 2);
 }
 bool rows_mfma_supported(int C, int64_t P) { return C >= 1 && C <= 16 && P % 32 == 0; }

@@ -40,7 +40,7 @@ struct MnlGeom {
   // two-workgroups-per-CU variant (tr_mnl_duo.hip): 4 waves, each owning every rank block of
   // one (i, j) block; LDS carve of ONE workgroup (floats)
   int duo;
-  int du_oZ, du_oP1, du_oG, du_oPF, du_lds_floats;
+  int du_oZ, du_oP1, du_oG, du_lds_floats;
   // bf16-split form of the duo family (k_mnl_bsp: a 32 KiB (128, 64) or (64, 128) sample at
   // rank <= 4, and every (32 NW, 64) sample with NW = 2..8 and (16 NW, 128) sample with NW = 4, 6,
   // 8 at rank <= 8 (other I, and J % 4 == 0 of 28..128, padded to the next), C <= 16; TR_DUO_SPLIT=1

@@ -35,18 +35,10 @@
 #include "tr_mnl.h"
 
 
-#ifndef TR_MNL_DMA_MEMCLOB
-#define TR_MNL_DMA_MEMCLOB 1  // "memory" clobber on the LDS-DMA asm (0: the compiler may move LDS reads across it)
-#endif
-#ifndef TR_MNL_SETPRIO
-#define TR_MNL_SETPRIO 0  // s_setprio 1 for waves 4-7 (MI355X_MICROARCH.md, two waves per SIMD item 4)
-#endif
-#ifndef TR_MNL_DMA_IN_GEMM
-#define TR_MNL_DMA_IN_GEMM 1  // issue the ring refill between GEMM steps instead of after the barrier
-#endif
-#ifndef TR_MNL_HOIST
-#define TR_MNL_HOIST 4  // operand quads of pair member a loaded before the previous pair's epilogue
-#endif
+// The ring refill is issued between GEMM steps (a burst after the barrier stalled on the memory
+// issue queue), and the first MN_HOIST operand quads of pair member a are loaded before the
+// previous pair's epilogue.
+constexpr int MN_HOIST = 4;
 #ifndef TR_MNL_PROFILE
 #define TR_MNL_PROFILE 0  // profiling build only: per-phase cycle counts of every wave of WG 0..255
 #endif
@@ -136,10 +128,7 @@ __device__ __forceinline__ void mn_dma16(const float* gsrc, const float* lds_dst
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
                : "=&s"(keep)
                : "v"(gsrc), "s"(a)
-#if TR_MNL_DMA_MEMCLOB
-               : "memory"
-#endif
-  );
+               : "memory");  // (without the clobber the compiler may move LDS reads across it)
 }
 // s_waitcnt vmcnt(n) for a wave-uniform runtime n (stricter than asked above 31: still safe)
 __device__ __forceinline__ void mn_wait_vm(int n) {
@@ -344,7 +333,7 @@ __device__ __forceinline__ void mnl_body(const MnlGeom& g, const MnArgs& a, cons
     if (ROLE == MN_ROLE_A) {
 #pragma unroll
       for (int c4 = 0; c4 < 16; ++c4) {
-        if (TR_MNL_DMA_IN_GEMM && dma_on && (c4 & 1) == 0 && (c4 >> 1) < gcnt) issue_at(dsrc, ddst, c4 >> 1);
+        if (dma_on && (c4 & 1) == 0 && (c4 >> 1) < gcnt) issue_at(dsrc, ddst, c4 >> 1);
         if (FULL || 4 * c4 < klen) {
           acc[0] = mfma_4x4(xr[c4].x, bop[4 * c4 + 0], acc[0]);
           acc[1] = mfma_4x4(xr[c4].y, bop[4 * c4 + 1], acc[1]);
@@ -373,7 +362,7 @@ __device__ __forceinline__ void mnl_body(const MnlGeom& g, const MnArgs& a, cons
     } else {
 #pragma unroll
       for (int st = 0; st < 16; ++st) {
-        if (TR_MNL_DMA_IN_GEMM && dma_on && (st & 1) == 0 && (st >> 1) < gcnt) issue_at(dsrc, ddst, st >> 1);
+        if (dma_on && (st & 1) == 0 && (st >> 1) < gcnt) issue_at(dsrc, ddst, st >> 1);
         if (FULL || 4 * st < klen) {
           acc[0] = mfma_4x4(xr[st].x, bop[st], acc[0]);
           acc[1] = mfma_4x4(xr[st].y, bop[st], acc[1]);
@@ -432,7 +421,7 @@ __device__ __forceinline__ void mnl_body(const MnlGeom& g, const MnArgs& a, cons
       const bool pre = k + nbuf - 1 < nr;  // refill slot (k - 1) % nbuf with sample k + nbuf - 1
       const int64_t npre = pre ? sample_of(k + nbuf - 1) : 0;
       const int bpre = (int)((k + nbuf - 1) % nbuf);
-      const bool pre_in_gemm = TR_MNL_DMA_IN_GEMM && ROLE != MN_ROLE_IDLE && k < nr;
+      const bool pre_in_gemm = ROLE != MN_ROLE_IDLE && k < nr;
       if (pre && !pre_in_gemm) {
 #pragma unroll
         for (int gi = 0; gi < kMnlGMax; ++gi)
@@ -511,13 +500,13 @@ __device__ __forceinline__ void mnl_body(const MnlGeom& g, const MnArgs& a, cons
       mn_barrier();  // every wave's pieces of pair p; Z partials of p - 1; slots of pair p - 1 free
       TR_MNL_MARK(1);
       const bool pre = p + nps - 1 < np;  // refill the slots of pair p - 1 with pair p + nps - 1
-      const bool pre_in_gemm = TR_MNL_DMA_IN_GEMM && ROLE != MN_ROLE_IDLE && p < np;
+      const bool pre_in_gemm = ROLE != MN_ROLE_IDLE && p < np;
       if (pre && !pre_in_gemm) issue_pair(p + nps - 1, slot_pre);
       const int pq = p + nps - 1;
       const int spre = 2 * slot_pre;
       TR_MNL_MARK(2);
-      float4 xra[16];  // member a's first TR_MNL_HOIST operand quads, in flight across the epilogue
-      constexpr int HO = FULL ? TR_MNL_HOIST : 0;
+      float4 xra[16];  // member a's first MN_HOIST operand quads, in flight across the epilogue
+      constexpr int HO = FULL ? MN_HOIST : 0;
       if (HO > 0 && ROLE != MN_ROLE_IDLE && p < np) load1(2 * slot_cur, xra, 0, HO);
       if (ROLE != MN_ROLE_IDLE) {
         if (p >= 1) {
@@ -631,9 +620,6 @@ __global__ __launch_bounds__(MN_T) void k_mnl_fused(MnlGeom g, MnArgs a, const i
   if (stop != nullptr && *stop != 0) return;
   const int lane = threadIdx.x & (TR_WAVE - 1);
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / TR_WAVE);  // wave-uniform
-#if TR_MNL_SETPRIO
-  if (wv >= MN_NW / 2) __builtin_amdgcn_s_setprio(1);  // the younger half loses VALU arbitration
-#endif
   if (wv < g.nA)
     mnl_body<MN_ROLE_A, FULL, SPI>(g, a, lab, class_w, lds, wv, lane);
   else if (wv < g.nunits)

@@ -16,9 +16,9 @@
 // What bounds it (round 5): the sample stream.  The timing ablations of round 4 kept the LDS-DMA
 // instructions (the "no DMA" build refilled the same, L2-resident sample) and so pointed at the
 // instruction stream; with the DMA removed entirely the bf16-split body below runs in 0.256 ms at
-// config 3 against 0.368 ms with it.  The non-temporal policy on the sample pieces (TR_DUO_NT, as
+// config 3 against 0.368 ms with it.  The non-temporal policy on the sample pieces (as
 // k_mnl_fused and k_linear_fused use) takes 6-7 % off both bodies (rank-block 0.364 -> 0.339 ms);
-// a second sample in flight per workgroup (TR_DUO_2IF) does not help at config 3 (two 4-wave
+// a second sample in flight per workgroup does not help at config 3 (two 4-wave
 // workgroups per CU already hold 128 KiB in flight).  The split body's one-workgroup-per-CU
 // shapes at 5 and 6 waves (80 / 96 KiB with two slots) do take a ring of three (+3-4 points).
 //
@@ -63,11 +63,6 @@ __device__ unsigned long long g_duo_prof[512][4][4];
   do {                  \
   } while (0)
 #endif
-#ifndef TR_DUO_P1REG
-#define TR_DUO_P1REG 1  // 1: the T unit's Phi1 operand quads held in 64 VGPRs for the launch (not read from
-                        // the LDS table every step: a third of the operand bytes), X addresses formed per
-                        // step, read-ahead 3 / 3 steps to fit 256 registers (the (128, 64) shape only)
-#endif
 #ifndef TR_DUO_SKIP
 #define TR_DUO_SKIP 0  // profiling ablation only (results invalid): 1 loop LDS-DMA, 2 MFMAs, 4 epilogue;
                        // bsp form: 8 no LDS-DMA at all after the first sample, 16 no label loads
@@ -78,51 +73,19 @@ namespace tr {
 namespace {
 constexpr int DU_NW = 4;
 constexpr int DU_T = DU_NW * TR_WAVE;
-#ifndef TR_DUO_XL
-#define TR_DUO_XL 6
-#endif
-constexpr int XL = TR_DUO_XL;  // GEMM steps an operand quad is read ahead of its MFMAs (B-waves)
-#ifndef TR_DUO_DMA_EVERY
-#define TR_DUO_DMA_EVERY 1
-#endif
-constexpr int DMA_EVERY = TR_DUO_DMA_EVERY;  // GEMM steps between the 8 LDS-DMA pieces of the next sample
-#ifndef TR_DUO_EARLY
-#define TR_DUO_EARLY 0
-#endif
-// 1: the LDS-DMA of sample k + 2 is issued as soon as every wave is past the GEMM of k (two
-// barriers per sample, up to two samples in flight per workgroup); 0: the DMA of k + 1 is
-// interleaved with the GEMM of k after the single barrier of iteration k
-constexpr bool EARLY = TR_DUO_EARLY != 0;
-#ifndef TR_DUO_XLA
-#define TR_DUO_XLA 4
-#endif
-constexpr int XLA = TR_DUO_XLA;  // the same for the A-waves (X and Phi1 quads)
-#ifndef TR_DUO_SB
-#define TR_DUO_SB 1
-#endif
-// 1: a scheduling fence after every GEMM step, so the operand reads stay XL / XLA steps ahead of
-// their MFMAs (left alone, the scheduler issues the T unit's reads one step ahead and waits on
-// them: exposed LDS latency in every step) and the epilogue stages stay between the steps
-constexpr bool SB = TR_DUO_SB != 0;
-#ifndef TR_DUO_PF
-#define TR_DUO_PF 0
-#endif
-#ifndef TR_DUO_IL
-#define TR_DUO_IL 0
-#endif
-// 1: workgroup b takes samples b, b + grid, b + 2 grid, ... (the chip streams one contiguous
-// front of X); 0: a contiguous range of rows_per_wg samples per workgroup
-constexpr bool IL = TR_DUO_IL != 0;
-// > 0: every lane of the workgroup pulls one 128-B line of sample k + PF into L2 during the GEMM
-// of k (one dword LDS-DMA into a scratch line per wave), so the LDS-DMA of that sample one
-// iteration later meets L2 / MALL latency instead of a loaded HBM round trip; 0: no prefetch
-constexpr int PF = TR_DUO_PF;
-#ifndef TR_DUO_2IF
-#define TR_DUO_2IF 0
-#endif
-// bsp form: 1 = two samples in flight per workgroup (sample k + 2 into slot k & 1 once every wave
-// holds its operands of k: a second barrier per sample); 0 = one (k + 1 into the other slot)
-constexpr bool TIF = TR_DUO_2IF != 0;
+// Kept from the round-2..5 experiments (each measured on one box against the build without it;
+// DESIGN.md "Two-workgroups-per-CU multinomial kernel" and "Multinomial, round 5"; the variants that
+// were not kept — early issue of sample k + 2, an L2 prefetch, interleaved sample order, two
+// samples in flight per workgroup — are in the git history):
+//  - rank-block body: operand quads read XL (V unit) / XLA (T unit) GEMM steps ahead of their MFMAs,
+//    and at (128, 64) the T unit's Phi1 quads held in 64 VGPRs for the launch (a third fewer
+//    operand bytes; read-ahead 3 / 3 to fit 256 registers; the (64, 128) shape would spill);
+//  - one LDS-DMA piece of the next sample per GEMM step (bursts stall the memory issue queue);
+//  - a scheduling fence after every GEMM step: the operand reads stay ahead of their MFMAs (left
+//    alone, the scheduler issues the T unit's reads one step ahead and waits on them) and the
+//    epilogue stages stay between the steps;
+//  - the non-temporal policy on the sample pieces (rank-block 0.364 -> 0.339 ms at c3).
+constexpr int XL = 6, XLA = 4;
 typedef float du_f32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ du_f32x4 du_mfma(float a, float b, du_f32x4 c) {
@@ -189,18 +152,6 @@ __device__ __forceinline__ du_f32x4 bs_mfma(sl_u4 a, const uint32_t (&b)[4], du_
 __device__ __forceinline__ uint32_t sl_pack_rne(float a, float b) {
   return __builtin_bit_cast(uint32_t, bs_bf2{(__bf16)a, (__bf16)b});
 }
-typedef _Float16 bs_h8 __attribute__((ext_vector_type(8)));
-typedef _Float16 bs_h2 __attribute__((ext_vector_type(2)));
-// two values -> one VGPR of packed round-to-nearest-even f16, v_cvt_pk_f16_f32
-__device__ __forceinline__ uint32_t bs_pack_h(float a, float b) {
-  return __builtin_bit_cast(uint32_t, bs_h2{(_Float16)a, (_Float16)b});
-}
-__device__ __forceinline__ du_f32x4 bs_mfma_h(sl_u4 a, const uint32_t (&b)[4], du_f32x4 c) {
-  if (TR_DUO_SKIP & 2) return c + __uint_as_float(a[0]) * __uint_as_float(b[0]);
-  const sl_u4 bb = sl_u4{b[0], b[1], b[2], b[3]};
-  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(bs_h8, a), __builtin_bit_cast(bs_h8, bb), c, 0, 0,
-                                                0);
-}
 __device__ __forceinline__ float sl_lo_f32(uint32_t h) { return __uint_as_float(__builtin_amdgcn_perm(h, h, 0x01000c0cu)); }
 __device__ __forceinline__ float sl_hi_f32(uint32_t h) { return __uint_as_float(h & 0xffff0000u); }
 // a (element 2m), b (element 2m + 1) -> three packed round-to-nearest pieces: x = x1 + x2 + x3 exactly
@@ -224,30 +175,12 @@ struct DuArgs {
   int reverse;
 };
 
-// L2 prefetch: one dword per lane from sbase + voff into the scratch LDS line at m0v (the value
-// is never read; only the line fill matters).  Counted by vmcnt like the LDS-DMA pieces.
-__device__ __forceinline__ void du_pf_s(uint32_t voff, const float* sbase, uint32_t m0v) {
-  uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dword %1, %2\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(voff), "s"(sbase), "s"(m0v)
-               : "memory");
-}
-
 // One LDS-DMA piece per lane with a scalar base: 16 B from sbase + voff (bytes, per lane) to LDS
 // byte address m0v + 16 * lane.  No per-piece 64-bit address arithmetic; m0 is compiler-reserved
 // and is saved / restored inside the statement.
-#ifndef TR_DUO_NT
-#define TR_DUO_NT 1  // non-temporal policy on the sample LDS-DMA (bsp at c3: 0.341 vs 0.364 ms)
-#endif
-#if TR_DUO_NT
-#define DU_NT " nt"
-#else
-#define DU_NT ""
-#endif
 __device__ __forceinline__ void du_dma_s(uint32_t voff, const float* sbase, uint32_t m0v) {
   uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" DU_NT "\n\ts_mov_b32 m0, %0"
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2 nt\n\ts_mov_b32 m0, %0"
                : "=&s"(keep)
                : "v"(voff), "s"(sbase), "s"(m0v)
                : "memory");
@@ -323,7 +256,7 @@ __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, cons
       (int)(uint32_t)(uintptr_t)((const __attribute__((address_space(3))) float*)lds));
   // LDS read offsets (floats): T quad c4 of this lane's row at aoff[c4]; V quad of step st at
   // boff[st & 3] + 4 J st; Phi1 quad of step st at pb + 4 st
-  constexpr bool P1R = TR_DUO_P1REG != 0 && JT == 64;  // (the (64, 128) shape spills one register with it)
+  constexpr bool P1R = JT == 64;  // (the (64, 128) shape spills one register with it)
   int aoff[P1R ? 1 : 16], boff[4];
   const int abase = (64 * ib + lane) * J + 64 * jb, c4s = 4 * c;  // (P1R: aoff of step st = abase + (c4s ^ 4 st))
   if constexpr (!P1R) {
@@ -333,15 +266,10 @@ __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, cons
 #pragma unroll
   for (int m = 0; m < 4; ++m) boff[m] = (64 * ib + grow) * J + 64 * jb + 4 * (c ^ (4 * m + grow));
   const int pb = rq * P1S + 64 * jb;
-  // prefetch: lane (wv, lane) touches line 64 wv + lane of the sample (256 lines = 32 KiB)
-  const uint32_t pfoff = 128u * (uint32_t)(wv * TR_WAVE + lane);
-  const uint32_t pfm0 = lbase + 4u * (uint32_t)g.du_oPF;
-
-  const int64_t n0 = IL ? (int64_t)blockIdx.x : (int64_t)blockIdx.x * a.rows_per_wg;
-  const int64_t G = IL ? (int64_t)gridDim.x : 1;
-  const int64_t n1 = IL ? a.N : (n0 + a.rows_per_wg < a.N ? n0 + a.rows_per_wg : a.N);
-  const int nr = (int)(n1 > n0 ? (n1 - n0 + G - 1) / G : 0);
-  auto sample_of = [&](int k) -> int64_t { return n0 + G * (a.reverse ? (nr - 1 - k) : k); };
+  const int64_t n0 = (int64_t)blockIdx.x * a.rows_per_wg;
+  const int64_t n1 = n0 + a.rows_per_wg < a.N ? n0 + a.rows_per_wg : a.N;
+  const int nr = (int)(n1 > n0 ? n1 - n0 : 0);
+  auto sample_of = [&](int k) -> int64_t { return n0 + (a.reverse ? (nr - 1 - k) : k); };
   auto src_of = [&](int k) -> const float* { return a.X + sample_of(k) * a.xld; };
 
   __syncthreads();
@@ -436,11 +364,7 @@ __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, cons
     for (int gi = 0; gi < 8; ++gi)
       du_dma_s(goff[gi], src, lbase + (uint32_t)(slot * 4 * SPF) + (uint32_t)(wv + DU_NW * gi) * 1024u);
   };
-  if (nr > 0) {
-    dma_sample(src_of(0), 0);
-    if (EARLY) dma_sample(src_of(nr > 1 ? 1 : 0), 1);
-    if (!EARLY && PF > 0) du_pf_s(pfoff, src_of(nr > 1 ? 1 : 0), pfm0);  // keeps the loop's vmcnt(1) exact
-  }
+  if (nr > 0) dma_sample(src_of(0), 0);
   int64_t yN = nr > 0 ? lab[sample_of(0)] : 0;  // label of the next GEMM sample (scalar, one ahead)
 
   // iteration k (ring slot SL = k & 1, a compile-time constant: the loop is unrolled by two so
@@ -456,12 +380,7 @@ __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, cons
     const int64_t yC = yN;
     const bool more = k + 1 < nr;
     yN = lab[sample_of(more ? k + 1 : k)];
-    if (EARLY)  // own pieces of sample k (those of k + 1, issued after them, may be in flight)
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (PF > 0)  // every piece of k; the prefetch of k + PF - 1 (issued after them) may be in flight
-      asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     TR_DUO_MARK(0);
     du_barrier();  // everyone's pieces of k; Z partials of k - 1; slot SL ^ 1 free
     TR_DUO_MARK(1);
@@ -494,10 +413,7 @@ __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, cons
     for (int st = 0; st < 16; ++st) {
       if (st + XLT < 16) ldT(st + XLT);
       if (st + XLV < 16) ldV(st + XLV);
-      if (!EARLY && st % DMA_EVERY == 0 && st / DMA_EVERY < 8)
-        du_dma_s(goff[st / DMA_EVERY], psrc, pm0 + (uint32_t)(st / DMA_EVERY) * 4096u);
-      if (!EARLY && PF > 0 && st == 8)
-        du_pf_s(pfoff, src_of(k + PF < nr ? k + PF : nr - 1), pfm0);
+      if (st < 8) du_dma_s(goff[st], psrc, pm0 + (uint32_t)st * 4096u);
       aT[0] = du_mfma(xt[st].x, bq[st].x, aT[0]);
       aT[1] = du_mfma(xt[st].y, bq[st].y, aT[1]);
       aT[2] = du_mfma(xt[st].z, bq[st].z, aT[2]);
@@ -507,7 +423,7 @@ __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, cons
       aV[2] = du_mfma(xv[st].z, bopB[st], aV[2]);
       aV[3] = du_mfma(xv[st].w, bopB[st], aV[3]);
       if ((st & 1) == 1 && st < 15) epi(1 + (st >> 1), SL ^ 1, yP, cwP);
-      if (SB) __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_sched_barrier(0);
     }
     TR_DUO_MARK(2);
     // T of sample k -> U partial of this unit -> Z partial (16 classes) -> LDS
@@ -535,13 +451,6 @@ __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, cons
     sZ[(SL * 16 + c) * 4 + rb + 2 * s] = zpart;
     yP = yC;
     cwP = cwC;
-    if (EARLY) {
-      // every wave is past the GEMM of k: slot SL takes sample k + 2 now, one wait + barrier
-      // earlier than the slot-free point of the interleaved scheme (a dummy refill of the last
-      // sample when there is none: vmcnt counts stay fixed)
-      du_barrier();
-      dma_sample(src_of(k + 2 < nr ? k + 2 : nr - 1), SL);
-    }
     TR_DUO_MARK(3);
   };
   for (int k = 0; k < nr; k += 2) {
@@ -607,11 +516,16 @@ __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, cons
 // ------------------------------------------------------------------------------------------
 // bf16-split form (g.bsp, the default where it fits): the same per-sample math on
 // v_mfma_f32_16x16x32_bf16 with the fp32 operands split into round-to-nearest bf16 pieces, as
-// the spectral slice kernel does (tr_spectral_slice.hip "bf16 split"): X in two pieces
-// (|x - x1 - x2| < 2^-16 |x|, unbiased), the factors in three, and the rank columns packed so
-// that one 16-wide MFMA carries every piece product of weight >= 2^-17:
+// the spectral slice kernel does (tr_spectral_slice.hip "bf16 split"): X and the factors each in
+// three pieces, x = x1 + x2 + x3 EXACTLY (x1 = bf16(x), x2 = bf16(x - x1), x3 = x - x1 - x2, at
+// most 8 significant bits; bf16 has fp32's exponent range, so this holds at any data scale), and
+// the rank columns packed so that 16-wide MFMAs carry every piece product of weight >= 2^-17:
 //   B12 = [b1 | b2] (columns 0-7 | 8-15, rank = column & 7), B3 = [b3 | 0]
-//   acc += x1.B12 + x2.B12 + x1.B3  ->  column r + column r + 8 = x1b1 + x1b2 + x2b1 + x2b2 + x1b3
+//   acc += x3.B12 + x2.B12 + x1.B3 + x1.B12  ->  column r + column r + 8
+//        = x1b1 + x1b2 + x2b1 + x2b2 + x1b3 + x3b1 + x3b2   (dropped: x2b3, x3b3, < 2^-24 |xb|)
+// (Round 5 carried x2 as ONE f16 piece of x - x1 against f16 factor pieces, three MFMAs: f16's
+// 5-bit exponent cost precision below |x| = 2^-5 (2e-4 relative at |x| ~ 1e-4) and overflowed to
+// inf above 2^24 — tests/test_gpu_parity.py::test_multinomial_split_body_x_scale.)
 // A 32 KiB sample takes 96 MFMAs per workgroup instead of 512 4x4x1 ones: the rank-block form
 // spends 1,024 issue cycles per wave-sample on MFMAs alone.  J = 64 samples of 32 NW rows run NW
 // waves (NW = 2..8), J = 128 ones of 16 NW rows NW waves (NW = 4, 6, 8); 8 / NW workgroups per
@@ -643,7 +557,7 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
   const int Ir = PAD ? g.I : I, Jr = PAD ? g.J : J;
   // NS = 3: a ring of three samples (the DMA of sample k + 2 goes into the slot of k - 1 while k
   // is computed: two samples in flight), where three fit the workgroup's LDS share
-  static_assert(NS == 2 || (NS == 3 && !TIF), "ring of two (optionally TIF) or three slots");
+  static_assert(NS == 2 || NS == 3, "ring of two or three slots");
   float* sU = lds + g.bs_oU;  // [NS slots][NW waves][8 ranks] U partials
   const float* P0 = a.phi;
   const float* P1 = a.phi + g.offP1;
@@ -665,17 +579,12 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
   const int iv0 = JT == 64 ? 32 * wv : 32 * (wv % NKS);           // V k-step (rows) of this wave
   const int cv = n + (J == 128 ? 16 * (wv / NKS) : 0);            // V chunk (j = 4 cv + tile)
   // B operands, split once per launch: T (Phi1, element e of lane group gq <-> j = 32 s + 8 gq + e)
-  uint32_t bT12[NKT][4], bT3[NKT][4], hT[NKT][4], bV12[4], bV3[4], hV[4];
-  auto bsplit = [&](float x0, float x1, uint32_t& b12, uint32_t& b3, uint32_t& hh) {
+  uint32_t bT12[NKT][4], bT3[NKT][4], bV12[4], bV3[4];
+  auto bsplit = [&](float x0, float x1, uint32_t& b12, uint32_t& b3) {
     uint32_t h1, h2, h3;
     sl_split2(x0, x1, h1, h2, h3);
     b12 = lo8 ? h1 : h2;
     b3 = lo8 ? h3 : 0u;
-    // f16 pieces for the sample's second piece: [f16(x) | f16(x - f16(x))]
-    const uint32_t f1 = bs_pack_h(x0, x1);
-    const bs_h2 f1v = __builtin_bit_cast(bs_h2, f1);
-    const uint32_t f2 = bs_pack_h(x0 - (float)f1v[0], x1 - (float)f1v[1]);
-    hh = lo8 ? f1 : f2;
   };
 #pragma unroll
   for (int s = 0; s < NKT; ++s)
@@ -683,13 +592,13 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
     for (int v = 0; v < 4; ++v) {
       const int j = 32 * s + 8 * gq + 2 * v;
       bsplit((rok && (!PAD || j < Jr)) ? P1[(int64_t)j * R + r8] : 0.f,
-             (rok && (!PAD || j + 1 < Jr)) ? P1[(int64_t)(j + 1) * R + r8] : 0.f, bT12[s][v], bT3[s][v], hT[s][v]);
+             (rok && (!PAD || j + 1 < Jr)) ? P1[(int64_t)(j + 1) * R + r8] : 0.f, bT12[s][v], bT3[s][v]);
     }
 #pragma unroll
   for (int v = 0; v < 4; ++v) {  // V (Phi0, element e <-> i = iv0 + 8 gq + e)
     const int i = iv0 + 8 * gq + 2 * v;
     bsplit((rok && (!PAD || i < Ir)) ? P0[(int64_t)i * R + r8] : 0.f,
-           (rok && (!PAD || i + 1 < Ir)) ? P0[(int64_t)(i + 1) * R + r8] : 0.f, bV12[v], bV3[v], hV[v]);
+           (rok && (!PAD || i + 1 < Ir)) ? P0[(int64_t)(i + 1) * R + r8] : 0.f, bV12[v], bV3[v]);
   }
   // U weights: T accumulator (lane (n, gq), reg v) = T[it0 + 16 tt + 4 gq + v][n & 7] after the
   // column fold; lanes n >= 8 hold the same values and weigh 0
@@ -841,11 +750,10 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
     for (int gi = 0; gi < 8; ++gi)
       dma_piece(goff[gi], src, lbase + (uint32_t)(slot * 4 * SPF) + (uint32_t)(wv + NW * gi) * 1024u);
   };
-  // two samples in flight per workgroup: sample k + 2 goes into slot k & 1 as soon as every wave
-  // holds its operands of k in registers (a second barrier per sample); the kernel is bound by the
-  // bytes in flight per CU, not by its issue stream (no-LDS-DMA ablation: 0.256 vs 0.368 ms at c3)
+  // the kernel is bound by the bytes in flight per CU, not by its issue stream (no-LDS-DMA
+  // ablation: 0.256 vs 0.368 ms at c3): a ring of three keeps two samples in flight
   if (nr > 0) dma_sample(src_of(0), 0);
-  if (nr > 0 && (TIF || NS == 3)) dma_sample(src_of(nr > 1 ? 1 : 0), 1);
+  if (nr > 0 && NS == 3) dma_sample(src_of(nr > 1 ? 1 : 0), 1);
   int64_t yN = nr > 0 ? lab[sample_of(0)] : 0;
 #if TR_DUO_PROFILE
   unsigned long long prof[4] = {0, 0, 0, 0};
@@ -857,7 +765,7 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
     const int64_t yC = yN;
     const bool more = k + 1 < nr;
     if (!(TR_DUO_SKIP & 16)) yN = lab[sample_of(more ? k + 1 : k)];
-    if (TIF || NS == 3)
+    if (NS == 3)
       asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // own pieces of k (those of k + 1 may be in flight)
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -866,10 +774,10 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
     TR_DUO_MARK(1);
     const float cwC = du_rdl(cwl, (int)yC);
     // sample k + 2 into this slot once it is read (past the end: a harmless refill of a valid sample)
-    const int kd = TIF ? k + 2 : k + NS - 1;  // the sample this iteration's DMA brings in
+    const int kd = k + NS - 1;  // the sample this iteration's DMA brings in
     constexpr int PS = (SL + NS - 1) % NS;     // slot of sample k - 1 (and of the DMA's target)
     const float* psrc = (kd < nr && !(TR_DUO_SKIP & 1)) ? src_of(kd) : src_of(nr - 1);
-    const uint32_t pm0 = lbase + (uint32_t)((TIF ? SL : PS) * 4 * SPF) + (uint32_t)wv * 1024u;
+    const uint32_t pm0 = lbase + (uint32_t)(PS * 4 * SPF) + (uint32_t)wv * 1024u;
     epi(0, PS, yP, cwP);
     const float* sb = lds + SL * SPF;
     du_f32x4 aT[NT], aV[4];
@@ -877,7 +785,7 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
     for (int q = 0; q < NT; ++q) aT[q] = du_f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int q = 0; q < 4; ++q) aV[q] = du_f32x4{0.f, 0.f, 0.f, 0.f};
-    // every operand of sample k into registers, then the slot is released (second barrier)
+    // every operand of sample k into registers
     constexpr int NU = NT * NKT;  // T steps (4); then 4 V steps (one j-tile each)
     du_f32x4 xv[8], xt[NU][2];
 #pragma unroll
@@ -889,39 +797,43 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
       xt[u][0] = *reinterpret_cast<const du_f32x4*>(sb + tro[tt] + 4 * (q0 ^ tsw));
       xt[u][1] = *reinterpret_cast<const du_f32x4*>(sb + tro[tt] + 4 * ((q0 + 1) ^ tsw));
     }
-    if (TIF) du_barrier();  // (its lgkmcnt(0): this wave's reads landed) every wave's operands of k read
 #pragma unroll
     for (int st = 0; st < NU + 4; ++st) {
       if (!(TR_DUO_SKIP & 8)) dma_piece(goff[st], psrc, pm0 + (uint32_t)st * (uint32_t)(NW * 1024));
-      sl_u4 x1, x2;
+      sl_u4 x1, x2, x3;  // the three exact pieces of the k step's X elements (pairs per VGPR)
       if (st < NU) {
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
           const du_f32x4& xr = xt[st][v >> 1];
-          const float e0 = xr[2 * (v & 1)], e1 = xr[2 * (v & 1) + 1];
-          const uint32_t h = sl_pack_rne(e0, e1);
-          x1[v] = h;
-          x2[v] = bs_pack_h(e0 - sl_lo_f32(h), e1 - sl_hi_f32(h));
+          uint32_t h1, h2, h3;
+          sl_split2(xr[2 * (v & 1)], xr[2 * (v & 1) + 1], h1, h2, h3);
+          x1[v] = h1;
+          x2[v] = h2;
+          x3[v] = h3;
         }
         const int tt = st / NKT, s = st - tt * NKT;
-        aT[tt] = bs_mfma_h(x2, hT[s], aT[tt]);
+        // smallest products first into the accumulator
+        aT[tt] = bs_mfma(x3, bT12[s], aT[tt]);
+        aT[tt] = bs_mfma(x2, bT12[s], aT[tt]);
         aT[tt] = bs_mfma(x1, bT3[s], aT[tt]);
         aT[tt] = bs_mfma(x1, bT12[s], aT[tt]);
       } else {
         const int tv = st - NU;  // j-tile: element tv of each row's chunk
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
-          const float e0 = xv[2 * v][tv], e1 = xv[2 * v + 1][tv];
-          const uint32_t h = sl_pack_rne(e0, e1);
-          x1[v] = h;
-          x2[v] = bs_pack_h(e0 - sl_lo_f32(h), e1 - sl_hi_f32(h));
+          uint32_t h1, h2, h3;
+          sl_split2(xv[2 * v][tv], xv[2 * v + 1][tv], h1, h2, h3);
+          x1[v] = h1;
+          x2[v] = h2;
+          x3[v] = h3;
         }
-        aV[tv] = bs_mfma_h(x2, hV, aV[tv]);
+        aV[tv] = bs_mfma(x3, bV12, aV[tv]);
+        aV[tv] = bs_mfma(x2, bV12, aV[tv]);
         aV[tv] = bs_mfma(x1, bV3, aV[tv]);
         aV[tv] = bs_mfma(x1, bV12, aV[tv]);
       }
       if (st >= 1 && st <= 7) epi(st, PS, yP, cwP);
-      if (SB) __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_sched_barrier(0);
     }
     TR_DUO_MARK(2);
     // fold the piece columns (rank r = column r + column r + 8), U partial of this wave -> LDS
@@ -1053,8 +965,6 @@ static int64_t duo_carve(MnlGeom* g, int nw, int64_t spf, int ns) {
   g->du_oP1 = (int)o;
   o += 8LL * (g->du_jt + 4);
   o = (o + 3) & ~(int64_t)3;
-  g->du_oPF = (int)o;  // prefetch scratch line (64 dwords, written by every wave, never read)
-  o += TR_WAVE;
   g->bs_oU = (int)o;  // bsp: [ns][NW waves][8 ranks] U partials
   o += ns * nw * 8;
   g->du_oG = g->slab <= ns * spf ? 0 : (int)o;  // the arena image aliases the drained ring
@@ -1112,9 +1022,8 @@ void mnl_duo_geom(MnlGeom* g) {
   // the split body at NW = 5, 6 (one workgroup per CU: 80 / 96 KiB in flight with two slots) takes
   // a ring of three samples: (160, 64) 58.9 -> 61.4 %, (192, 64) 65.4 -> 68.5 %, (96, 128) 65.8 ->
   // 69.7 % of HBM (tools/mnl_shapes.py, two runs each); at NW = 3 (two workgroups per CU) three
-  // slots measured the same as two.  TR_DUO_RING=2 keeps two.
-  const char* ring = std::getenv("TR_DUO_RING");
-  const bool ring3_ok = bsp && (nw == 5 || nw == 6) && (jt == 64 || nw == 6) && !(ring != nullptr && ring[0] == '2');
+  // slots measured the same as two.
+  const bool ring3_ok = bsp && (nw == 5 || nw == 6) && (jt == 64 || nw == 6);
   int ns = 2;
   if (ring3_ok && wpc * carve(3) * 4 <= 160 * 1024) ns = 3;
   const int64_t o = carve(ns);
@@ -1166,7 +1075,9 @@ hipError_t mnl_duo_prepare(MnlGeom* g) {
     g->du_nw = 4;
     g->du_wpc = 2;
     g->du_ns = 2;
+    g->du_pad = 0;
     g->du_jt = g->J;
+    g->du_lds_floats = (int)duo_carve(g, 4, 8192, 2);  // its own carve (the split body's may differ)
     e = duo_kernel_ok(*g, &ok);
     if (e != hipSuccess) return e;
     if (ok) return hipSuccess;

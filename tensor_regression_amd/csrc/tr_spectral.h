@@ -44,7 +44,7 @@ struct SpecGeom {
   int sl;                       // 1: SPEC_TRAIN runs k_spec_slice
   int slSp;                     // its GEMMs: 0 f32 MFMA; bf16 split with X in two pieces: 1 lin packed, 2 not; X in three: 3, 4
   int slDt, sl_Dp;              // rows d >= 128 (<= 2), rows of the phi(A1) / phi(C1) tables
-  int sl_oTail, sl_oEx, sl_oTP, sl_oPart, sl_oN1, sl_oLoss, sl_oPF, sl_lds_floats;  // LDS carve (floats)
+  int sl_oTail, sl_oEx, sl_oTP, sl_oPart, sl_oN1, sl_oLoss, sl_lds_floats;  // LDS carve (floats)
 };
 
 // Fills g; returns false (with a reason) when the shape is outside the kernels' envelope.

@@ -46,63 +46,17 @@
 #define TR_SLICE_SKIP 0  // timing ablation only (results invalid): 1 no LDS-DMA after the first sample,
                          // 2 no forward MFMAs, 4 no gradient MFMAs
 #endif
-#ifndef TR_SLICE_PRIO
-#define TR_SLICE_PRIO 1  // s_setprio 1 for the second-dispatched half (waves 4-7); 2: for the first half
-#endif
-#ifndef TR_SLICE_BPF
-#define TR_SLICE_BPF 1  // gradient GEMM: next tile's operand reads issued before this tile's MFMAs
-#endif
-#ifndef TR_SLICE_NT
-#define TR_SLICE_NT 0  // non-temporal policy on the slice LDS-DMA (off: neighbour pairs share row lines in L2; nt gave 1.29x HBM traffic, default 1.05x)
-#endif
-#if TR_SLICE_NT
-#define SL_NT " nt"
-#else
-#define SL_NT ""
-#endif
-#ifndef TR_SLICE_PF
-#define TR_SLICE_PF 0  // split kernels: L2 prefetch of the next sample, dword LDS-DMA pieces per wave
-                       // (64 lanes at a TR_SLICE_PFS-byte stride) into a discarded LDS line
-#endif
-#ifndef TR_SLICE_PFS
-#define TR_SLICE_PFS 128  // prefetch stride (bytes); TR_SLICE_PF * 64 * 8 * stride covers the sample
-#endif
-#ifndef TR_SLICE_PFAT
-#define TR_SLICE_PFAT 0  // 0: prefetch at the top of the sample (before the forward), 1: after the forward
-#endif
-#ifndef TR_SLICE_BKW
-#define TR_SLICE_BKW 4  // wave that keeps the per-sample bookkeeping (dA2 / dC2 / bias / loss / y_hat,
-                        // tail-row sums): a second-half wave, off the first half's critical path
-#endif
-#ifndef TR_SLICE_TAILLAST
-#define TR_SLICE_TAILLAST 1  // split kernels: the tail column's dword LDS-DMA goes out after the sample's
-                             // 16 tile pieces (its 128-B lines are then already on their way into L2)
-                             // instead of before them (0: every tail dword was its own HBM sector miss)
-#endif
-#ifndef TR_SLICE_TAILAT
-#define TR_SLICE_TAILAT 1  // with TAILLAST: wave p issues its tail dwords right after its pieces of gradient
-                           // tile TQ p + TQ - 1 (the tiles holding its tail rows, whose 128-B lines the
-                           // pair waves 0 / 3 fetch at the same stage) instead of after tile 7
-#endif
-#ifndef TR_SLICE_TAILQ
-#define TR_SLICE_TAILQ -1  // >= 0: every wave issues its tail after tile TR_SLICE_TAILQ (one code copy)
-#endif
-#ifndef TR_SLICE_TAILBUF
-#define TR_SLICE_TAILBUF 1  // split kernels: the tail dwords through the sample's buffer descriptor, all 64
-                            // lanes (no lane branch, no 64-bit per-lane address)
-#endif
-#ifndef TR_SLICE_TAILMASK
-#define TR_SLICE_TAILMASK 1  // TAILBUF: lanes past the Dt tail rows take an out-of-range offset (no request;
-                             // each active lane's dword is a line of its own in the memory pipeline)
-#endif
-#ifndef TR_SLICE_NOSEL
-#define TR_SLICE_NOSEL 1  // epilogue table reads without per-element lane masks (see tab8)
-#endif
-#ifndef TR_SLICE_AHEAD
-#define TR_SLICE_AHEAD 1  // split kernels (with TR_SLICE_BPF): the next sample's pieces of gradient tile q + 1
-                          // go out at tile q (its reads have landed there), a tile earlier
-#endif
-static_assert(!TR_SLICE_AHEAD || TR_SLICE_BPF, "TR_SLICE_AHEAD needs the next tile's reads issued a tile ahead");
+// Kept from the round-2..5 experiments (each measured on one box against the build without it,
+// DESIGN.md "Spectral kernels"; the variants that were not kept are in the git history):
+//  - the second-dispatched half (waves 4-7) runs at s_setprio 1;
+//  - the gradient GEMM issues the next tile's operand reads before this tile's MFMAs, and the next
+//    sample's pieces of tile q + 1 at tile q (as soon as those reads have landed);
+//  - the per-sample bookkeeping (dA2 / dC2 / bias / loss / y_hat, tail-row sums) on a second-half
+//    wave (SL_BKW), off the first half's critical path;
+//  - split kernels: the tail column's dwords go out through the sample's buffer descriptor (all 64
+//    lanes, lanes past the Dt tail rows masked by an out-of-range offset) right after the wave's
+//    pieces of the tiles that hold its tail rows (their 128-B lines are then on their way into L2);
+//  - the epilogue's table reads carry no per-element lane masks (see tab8).
 #ifndef TR_SLICE_PROFILE
 #define TR_SLICE_PROFILE 0  // profiling build: per-phase cycle counts of wave 0 of workgroups 0..255
 #endif
@@ -141,6 +95,7 @@ constexpr int SL_SLICE = SL_ROWS * 32;  // floats of one wave's slice
 constexpr int SL_STEPS = SL_ROWS / 4;   // forward k steps per wave
 constexpr int SL_TILES = SL_ROWS / 16;  // gradient w tiles per wave
 constexpr int SL_TAIL = 64;             // tail floats per wave (Dt <= 2 rows x <= 32 w)
+constexpr int SL_BKW = 4;               // the bookkeeping wave (a second-half wave)
 // fixed part of the LDS carve (floats): slices, tails, exchange, tail partials, column partials;
 // compile-time in the kernel (held as run-time values they took scalar registers the sample loop
 // spilled); spec_slice_geom lays the same carve out
@@ -324,7 +279,7 @@ __device__ __forceinline__ uint32_t sl_lds_addr(const float* p) {
 __device__ __forceinline__ void sl_dma16bq(__amdgpu_buffer_rsrc_t rs, uint32_t tstr, uint32_t q, uint32_t voff,
                                            uint32_t lds_b, uint32_t lds_off) {
   uint32_t keep, so;
-  asm volatile("s_mul_i32 %1, %4, %5\n\ts_mov_b32 %0, m0\n\ts_add_u32 m0, %3, %7\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %6, %1 offen" SL_NT " lds\n\ts_mov_b32 m0, %0"
+  asm volatile("s_mul_i32 %1, %4, %5\n\ts_mov_b32 %0, m0\n\ts_add_u32 m0, %3, %7\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %6, %1 offen lds\n\ts_mov_b32 m0, %0"
                : "=&s"(keep), "=&s"(so)
                : "v"(voff), "s"(lds_b), "s"(tstr), "s"(q), "s"(rs), "s"(lds_off)
                : "memory", "scc");
@@ -332,7 +287,7 @@ __device__ __forceinline__ void sl_dma16bq(__amdgpu_buffer_rsrc_t rs, uint32_t t
 // one 4-B LDS-DMA piece per lane: gsrc -> LDS byte address m0 + 4 * lane (m0 saved / restored)
 __device__ __forceinline__ void sl_dma4(const float* gsrc, const float* lds_dst) {
   uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off" SL_NT "\n\ts_mov_b32 m0, %0"
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
                : "=&s"(keep)
                : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(sl_lds_addr(lds_dst)))
                : "memory");
@@ -340,7 +295,7 @@ __device__ __forceinline__ void sl_dma4(const float* gsrc, const float* lds_dst)
 // one 16-B LDS-DMA piece per lane: gsrc (4-B aligned is enough) -> LDS byte address m0 + 16 * lane
 __device__ __forceinline__ void sl_dma16(const float* gsrc, const float* lds_dst) {
   uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" SL_NT "\n\ts_mov_b32 m0, %0"
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                : "=&s"(keep)
                : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(sl_lds_addr(lds_dst)))
                : "memory");
@@ -353,14 +308,14 @@ __device__ __forceinline__ void sl_dma16(const float* gsrc, const float* lds_dst
 // the descriptor's range reads 0
 __device__ __forceinline__ void sl_dma4b(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t lds_b) {
   uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen" SL_NT " lds\n\ts_mov_b32 m0, %0"
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
                : "=&s"(keep)
                : "v"(voff), "s"(rs), "s"(lds_b)
                : "memory");
 }
 __device__ __forceinline__ void sl_dma16b(__amdgpu_buffer_rsrc_t rs, uint32_t soff, uint32_t voff, uint32_t lds_b) {
   uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen" SL_NT " lds\n\ts_mov_b32 m0, %0"
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
                : "=&s"(keep)
                : "v"(voff), "s"(rs), "s"(lds_b), "s"(soff)
                : "memory");
@@ -417,9 +372,6 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
   constexpr int SQ = TR / 4;   // ... = forward steps [SQ p, SQ (p + 1))
   const int wbase = hw * WH;   // first w of this wave's half
   const int dbase = 32 * p;    // first d of this wave's pair
-  const int rs = i / CC;       // spectral rank of this lane's column (tile 0)
-  const bool rs_ok = rs < Rs;
-  const bool vlane = rs_ok && (i % CC) == 0;  // lane that carries V / dPhi(C1) of rank rs
 
   float* slice = lds + wv * SL_SLICE;
   const uint32_t slice_b = (uint32_t)__builtin_amdgcn_readfirstlane(sl_lds_addr(slice));  // its LDS byte address
@@ -568,59 +520,40 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
   };
   auto dma_tail = [&](int64_t n) {
     const int ln = sl_lane_now();  // the per-lane source is formed at the call (no live address pair)
-    if (SP && TR_SLICE_TAILBUF) {
-      // lane -> (row 128 + lane / TR, w offset lane % TR) as below; lanes with lane / TR >= Dt read
-      // 0 (TR_SLICE_TAILMASK) or the next row's first columns into tail slots nothing reads
+    if (SP) {
+      // through the sample's descriptor, all 64 lanes: lane -> (row 128 + lane / TR, w offset
+      // lane % TR) as below; lanes with lane / TR >= Dt take an out-of-range offset (no request:
+      // each active lane's dword is a line of its own in the memory pipeline)
       const int tr = ln / TR, wo = ln - tr * TR;
       const uint32_t off = (uint32_t)(((TR * p + wo) * D + 128 + tr) * 4);
-      sl_dma4b(rsrc_of(n), (TR_SLICE_TAILMASK && tr >= Dt) ? 0xFFFFFF00u : off, tail_b);
+      sl_dma4b(rsrc_of(n), tr >= Dt ? 0xFFFFFF00u : off, tail_b);
     } else if (ln < Dt * TR) {  // lane -> (row 128 + lane / TR, w offset lane % TR)
       const int tr = ln / TR, wo = ln - tr * TR;
       const int64_t w = wbase + TR * p + wo;
       sl_dma4(X + n * xld + (w < g.W ? w : 0) * D + 128 + tr, sTail);  // (rows past W: any valid row, times zero)
     }
   };
-  // split kernels (TR_SLICE_TAILLAST): the tail goes last, after every tile piece of the sample;
-  // otherwise first (waiting for tile 0 also retires it: the f32 form reads it inside the loop)
-  constexpr bool TAIL_LAST = SP && TR_SLICE_TAILLAST;
-  constexpr int NTL = (TAIL_LAST && Dt > 0) ? 1 : 0;  // tail pieces issued after the tiles
-  // TR_SLICE_TAILAT: after tile qt instead (the forward's wait for tile q + 1 then counts the tail
-  // only while q + 1 <= qt)
-  constexpr bool TAIL_AT = TAIL_LAST && TR_SLICE_TAILAT;
-  const int qt = !TAIL_AT ? SL_TILES - 1 : TR_SLICE_TAILQ >= 0 ? TR_SLICE_TAILQ : TQ * p + TQ - 1;
+  // split kernels: wave p's tail goes out right after its pieces of tile qt = TQ p + TQ - 1 (the
+  // tiles holding its tail rows, whose 128-B lines the pair waves 0 / 3 fetch at the same stage;
+  // the forward's wait for tile q + 1 counts the tail only while q + 1 <= qt); the f32 form issues
+  // it first (waiting for tile 0 also retires it: it reads the tail inside the loop)
+  constexpr bool TAIL_LAST = SP;
+  constexpr int NTL = (TAIL_LAST && Dt > 0) ? 1 : 0;  // tail pieces issued after tile pieces
+  const int qt = !TAIL_LAST ? SL_TILES - 1 : TQ * p + TQ - 1;
   auto dma_sample = [&](int64_t n) {
     if (Dt > 0 && !TAIL_LAST) dma_tail(n);
 #pragma unroll
     for (int q = 0; q < SL_TILES; ++q) {
       dma_tile(n, q);
-      if (Dt > 0 && TAIL_AT && q == qt) dma_tail(n);
+      if (Dt > 0 && TAIL_LAST && q == qt) dma_tail(n);
     }
-    if (Dt > 0 && TAIL_LAST && !TAIL_AT) dma_tail(n);
   };
 
   __builtin_amdgcn_s_waitcnt(0);  // retire the prologue's loads (the loop's waits are counted)
   __syncthreads();
-  // L2 prefetch of sample n: wave wv touches the 128-B lines (2 wv + pc) * 64 + lane, pc < TR_SLICE_PF,
-  // of the sample's W * D floats (one dword each, landing in a shared scratch LDS line that nothing
-  // reads): the sample's HBM transfer then overlaps this sample's forward and epilogue, and its
-  // LDS-DMA in the gradient GEMM reads L2.  (The LDS holds one sample: without it the next
-  // sample's transfer could only overlap the gradient GEMM.)
-  constexpr int NPF = SP ? TR_SLICE_PF : 0;
-  auto prefetch = [&](int64_t n) {
-    const int ln = sl_lane_now();
-    const int64_t sbytes = (int64_t)g.W * D * 4;
-    const char* base = reinterpret_cast<const char*>(X + n * xld);
-#pragma unroll
-    for (int pc = 0; pc < NPF; ++pc) {
-      int64_t off = ((int64_t)((NPF * wv + pc) * 64 + ln)) * TR_SLICE_PFS;
-      off = off < sbytes ? off : sbytes - 4;
-      sl_dma4(reinterpret_cast<const float*>(base + off), lds + g.sl_oPF);
-    }
-  };
   set_dvo();
   if (nr > 0) dma_sample(sample_of(0));
-  if (TR_SLICE_PRIO == 1 && hw == 1) __builtin_amdgcn_s_setprio(1);
-  if (TR_SLICE_PRIO == 2 && hw == 0) __builtin_amdgcn_s_setprio(1);
+  if (hw == 1) __builtin_amdgcn_s_setprio(1);
 #if TR_SLICE_PROFILE
   unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long prof_t = __builtin_readcyclecounter();
@@ -631,9 +564,6 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
     const int64_t n = sample_of(k);
     const bool has_next = k + 1 < nr && !((TR_SLICE_SKIP & 1) && k > 0);
     const int64_t nn = has_next ? sample_of(k + 1) : n;
-    // pieces issued below this sample's DMA (the forward's counted waits allow for them)
-    const int npf = (NPF > 0 && has_next && !TR_SLICE_PFAT) ? NPF : 0;
-    if (npf > 0) prefetch(nn);
 
     // ---- forward: T (tile jt, d tile h) over this wave's half ---------------------------
     sl_f4 T00 = {0.f, 0.f, 0.f, 0.f}, T01 = T00, T10 = T00, T11 = T00;
@@ -652,7 +582,7 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
       }
       {
         SL_SUB_BEGIN();
-        sl_wait_vm((ntl - 1) * 2 + NTL + npf);
+        sl_wait_vm((ntl - 1) * 2 + NTL);
         SL_SUB_END(1);
       }
 #pragma unroll
@@ -662,7 +592,7 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
         if (q + 1 < ntl) {
           {
             SL_SUB_BEGIN();
-            sl_wait_vm((ntl - 2 - q) * 2 + (q + 1 <= qt ? NTL : 0) + npf);
+            sl_wait_vm((ntl - 2 - q) * 2 + (q + 1 <= qt ? NTL : 0));
             SL_SUB_END(1);
           }
 #pragma unroll
@@ -715,7 +645,6 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
         for (int s = 0; s < 4; ++s) xa[s] = xb[s];
       }
     }
-    if (TR_SLICE_PFAT && NPF > 0 && has_next) prefetch(nn);
     // y of the first two outputs by scalar loads issued here: their latency hides under the
     // exchange, barrier A and the column partials (issued inside the output loop it was exposed;
     // issued before the forward, an SMEM load in flight turns its counted LDS waits into lgkmcnt(0))
@@ -741,7 +670,7 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
         // (rows >= Dt zero), element j <-> w offset 4 j + gq of the wave's 32 tail w (after the
         // loop: nothing of the forward is live; one case per static S)
         sl_u4 tf[3];
-        if (NTL) sl_wait_vm(npf);  // the tail (issued after the tiles) has landed
+        if (NTL) sl_wait_vm(0);  // the tail (issued after the tiles) has landed
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
           const float x0 = i < Dt ? sTail[i * TR + 8 * m + gq] : 0.f;
@@ -815,24 +744,24 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
     // phi(A1)[d, ie] / phi(C1)[d, ie / CC] of this lane's 8 rows d = dbase + 8 ge + 2v + h: two
     // ds_read_b128 each, element 2v + h
     const int n1o = (ie < Rn ? ie : 0) * Dp + dbase + 8 * ge, c1o = (rse < Rs ? rse : 0) * Dp + dbase + 8 * ge;
-    // (TR_SLICE_NOSEL: no per-element lane masks; a lane past Rn / Rs reads table row 0, finite,
+    // (no per-element lane masks; a lane past Rn / Rs reads table row 0, finite,
     // and meets zero factors: T columns past Rn are zero, and dz / dv are zeroed there, so only
     // the lin column partial needs one mask — the packed form's lanes 8-15 hold folded columns)
-    auto tab8 = [&](const float* tb, int off, bool ok, float (&o)[2][4]) {
+    auto tab8 = [&](const float* tb, int off, float (&o)[2][4]) {
       const sl_f4 lo = *reinterpret_cast<const sl_f4*>(tb + off), hi = *reinterpret_cast<const sl_f4*>(tb + off + 4);
 #pragma unroll
       for (int v = 0; v < 4; ++v)
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const float x = v < 2 ? lo[2 * v + h] : hi[2 * (v - 2) + h];
-          o[h][v] = (TR_SLICE_NOSEL || ok) ? x : 0.f;
+          o[h][v] = x;
         }
     };
     float zp = 0.f, vp = 0.f;
     {
       float n1[2][4], c1[2][4];
-      tab8(sN1, n1o, i < Rn, n1);
-      tab8(sC1, c1o, rs_ok, c1);
+      tab8(sN1, n1o, n1);
+      tab8(sC1, c1o, c1);
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -842,14 +771,14 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
         vp = fmaf(hw == 0 ? c1[0][v] : c1[1][v], norm_of(hw == 0 ? T00[v] : T01[v]), vp);
     }
     vp = vlane ? vp : 0.f;
-    if (TR_SLICE_NOSEL) zp = i < Rn ? zp : 0.f;
+    zp = i < Rn ? zp : 0.f;
     const float Mt = norm_of(tt0);
     const int dtl = 128 + gq;  // tail row of this lk group (valid when gq < Dt)
     const float n1t = (Dt > 0 && gq < Dt && i < Rn) ? sN1[i * Dp + dtl] : 0.f;
     const float c1t = (Dt > 0 && gq < Dt && rs_ok) ? sC1[rs * Dp + dtl] : 0.f;
     zp = sl_groups_sum(zp);
     vp = sl_groups_sum(vp);
-    if (wv == TR_SLICE_BKW && Dt > 0) {  // the bookkeeping wave adds the tail rows' terms
+    if (wv == SL_BKW && Dt > 0) {  // the bookkeeping wave adds the tail rows' terms
       float zt = n1t * tt1;
       float vt = vlane ? c1t * Mt : 0.f;
       zp += sl_groups_sum(zt);
@@ -865,8 +794,8 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
 
     // ---- Z / V, y_hat, residual, dZ / dV (every wave, identical order) ----------------------
     float n1[2][4], c1[2][4];  // (issued first: their latency hides under the sums below)
-    tab8(sN1, n1o, i < Rn, n1);
-    tab8(sC1, c1o, rs_ok, c1);
+    tab8(sN1, n1o, n1);
+    tab8(sC1, c1o, c1);
     const float zi = sl_sum8(sPart + i * SL_NW), vi = sl_sum8(sPart + (16 + i) * SL_NW);
     float dz = 0.f, dv = 0.f;
     // output o with target yo: y_hat, residual, its dZ / dV terms, the bookkeeping wave's sums
@@ -880,7 +809,7 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
       const float rv = e * scale;
       dz = fmaf(rv, ca, dz);
       dv = fmaf(rv, sCC[o * 16 + rs], dv);
-      if (wv == TR_SLICE_BKW && lk < 16) {
+      if (wv == SL_BKW && lk < 16) {
         if (i < Rn) sAcc[o * Rn + i] += sWt[i] * rv * zi;
         if (i < Rs) sAcc[NO * Rn + o * Rs + i] += rv * vi;
         if (lk == 0) {
@@ -924,7 +853,7 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
     if (Dt > 0) {
       dTt1 = dz * n1t;
       dTt0 = Mt > 0.f ? dv * c1t * __builtin_amdgcn_rcpf(Mt) * tt0 : 0.f;
-      if (wv == TR_SLICE_BKW && gq < Dt) {
+      if (wv == SL_BKW && gq < Dt) {
         if (i < Rn) sTacc[gq * 32 + i] = fmaf(dz, tt1, sTacc[gq * 32 + i]);
         if (vlane) sTacc[gq * 32 + 16 + rs] = fmaf(dv, Mt, sTacc[gq * 32 + 16 + rs]);
       }
@@ -968,25 +897,16 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
           }
         }
       }
-      sl_f4 pa, pb;
-      if (TR_SLICE_BPF) {
-        pa = *reinterpret_cast<const sl_f4*>(slice + bo0);
-        pb = *reinterpret_cast<const sl_f4*>(slice + bo1);
-      }
+      // the next tile's operand reads go out before this tile's MFMAs
+      sl_f4 pa = *reinterpret_cast<const sl_f4*>(slice + bo0);
+      sl_f4 pb = *reinterpret_cast<const sl_f4*>(slice + bo1);
 #pragma unroll
       for (int q = 0; q < SL_TILES; ++q) {
         if (q < ntl) {
-          sl_f4 va, vb;
-          if (TR_SLICE_BPF) {
-            va = pa;
-            vb = pb;
-            if (q + 1 < ntl) {
-              pa = *reinterpret_cast<const sl_f4*>(slice + 512 * (q + 1) + bo0);
-              pb = *reinterpret_cast<const sl_f4*>(slice + 512 * (q + 1) + bo1);
-            }
-          } else {
-            va = *reinterpret_cast<const sl_f4*>(slice + 512 * q + bo0);
-            vb = *reinterpret_cast<const sl_f4*>(slice + 512 * q + bo1);
+          const sl_f4 va = pa, vb = pb;
+          if (q + 1 < ntl) {
+            pa = *reinterpret_cast<const sl_f4*>(slice + 512 * (q + 1) + bo0);
+            pb = *reinterpret_cast<const sl_f4*>(slice + 512 * (q + 1) + bo1);
           }
           // the tile's two LDS-DMA pieces of the next sample go out between its MFMAs (after
           // the reads landed), not back to back: bursts stall on the memory issue queue
@@ -1003,7 +923,7 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
               }
               if (has_next && (v & 1)) {
                 if (v == 1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // tile q's reads landed
-                // (with TR_SLICE_BPF the next tile's two reads may still be in flight: waited too)
+                // (the next tile's two reads may still be in flight: waited too)
                 dma_piece(nn, q, v >> 1);
               }
             }
@@ -1015,32 +935,22 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
               const sl_f4& src = v < 2 ? va : vb;
               sl_splitx_m<SL_XP(SP)>(src[2 * (v & 1) + 0], src[2 * (v & 1) + 1], af, v);
             }
-            if (TR_SLICE_AHEAD) {
-              // the reads of tile q and (TR_SLICE_BPF) q + 1 have landed at this wait: the next
-              // sample's pieces of tile q + 1 go out now, a tile earlier (tile 0's at q = 0); the
-              // issue order (tiles in order, the tail after tile qt) is the forward's count
-              if (has_next) {
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                if (q == 0) {
-                  dma_piece(nn, 0, 0);
-                  dma_piece(nn, 0, 1);
-                  if (TAIL_AT && Dt > 0 && qt == 0) dma_tail(nn);
-                }
-                if (q + 1 < ntl) dma_piece(nn, q + 1, 0);
+            // the reads of tile q and q + 1 have landed at this wait: the next sample's pieces of
+            // tile q + 1 go out now, a tile earlier (tile 0's at q = 0); the issue order (tiles in
+            // order, the tail after tile qt) is the forward's count
+            if (has_next) {
+              asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+              if (q == 0) {
+                dma_piece(nn, 0, 0);
+                dma_piece(nn, 0, 1);
+                if (TAIL_LAST && Dt > 0 && qt == 0) dma_tail(nn);
               }
-              if (!(TR_SLICE_SKIP & 4)) gacc[q][0] = sl_mfma6<SL_XP(SP)>(af, ds, gacc[q][0]);
-              if (has_next && q + 1 < ntl) {
-                dma_piece(nn, q + 1, 1);
-                if (TAIL_AT && Dt > 0 && q + 1 == qt) dma_tail(nn);
-              }
-            } else {
-              if (has_next) {
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // tile q's reads landed
-                dma_piece(nn, q, 0);
-              }
-              if (!(TR_SLICE_SKIP & 4)) gacc[q][0] = sl_mfma6<SL_XP(SP)>(af, ds, gacc[q][0]);
-              if (has_next) dma_piece(nn, q, 1);
-              if (TAIL_AT && has_next && Dt > 0 && q == qt) dma_tail(nn);
+              if (q + 1 < ntl) dma_piece(nn, q + 1, 0);
+            }
+            if (!(TR_SLICE_SKIP & 4)) gacc[q][0] = sl_mfma6<SL_XP(SP)>(af, ds, gacc[q][0]);
+            if (has_next && q + 1 < ntl) {
+              dma_piece(nn, q + 1, 1);
+              if (TAIL_LAST && Dt > 0 && q + 1 == qt) dma_tail(nn);
             }
             if (!(TR_SLICE_SKIP & 4)) {
               if constexpr (SL_LP(SP))
@@ -1055,8 +965,6 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
           }
         }
       }
-      // (this wave's tail operands were read at the top of the phase, and its tile reads waited)
-      if (TAIL_LAST && !TAIL_AT && has_next && Dt > 0) dma_tail(nn);
     }
     SL_MARK(7);
   }
@@ -1169,8 +1077,7 @@ void spec_slice_geom(SpecGeom* g) {
   const int64_t small = (int64_t)g->sl_Dp * (g->Rn + g->Rs) + (int64_t)g->NO * 33 + 16 +
                         (int64_t)g->NO * (g->Rn + g->Rs + 1) + 2 * 32;
   g->sl_oLoss = (int)(g->sl_oN1 + ((small + 3) & ~(int64_t)3));  // 16-B aligned double
-  g->sl_oPF = g->sl_oLoss + 4;  // 64 floats (with TR_SLICE_PF): landing line of the L2 prefetch (never read)
-  const int64_t tot = g->sl_oPF + (TR_SLICE_PF > 0 ? 64 : 0);
+  const int64_t tot = g->sl_oLoss + 4;
   if (tot * 4 > 160 * 1024) return;
   g->sl_lds_floats = (int)tot;
   g->sl = 1;

@@ -40,10 +40,7 @@ __device__ int g_upd_launch;
 
 namespace {
 constexpr int UPD_T = 1024;  // threads of the one workgroup (the norm order above assumes it)
-#ifndef TR_UPD_TRIP
-#define TR_UPD_TRIP 2
-#endif
-constexpr int UPD_TRIP = TR_UPD_TRIP;  // elements per thread per loop trip (loads in flight together)
+constexpr int UPD_TRIP = 2;  // elements per thread per loop trip (loads in flight together; 4: no better)
 
 __device__ __forceinline__ int factor_of(const FactorSet& fs, int64_t e) {
   int f = 0;

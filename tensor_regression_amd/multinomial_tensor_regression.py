@@ -180,11 +180,15 @@ class CP_logistic_regression():
         cdev = _engine.collective_device(process_group)
         y = torch.as_tensor(self.y).reshape(-1).to(cdev, torch.long)
         n = y.numel()
-        rng = torch.tensor([int(y.max()) if n else -1, -int(y.min()) if n else 0, n], dtype=torch.int64, device=cdev)
-        nn_ = rng[2:].clone()
+        # label range and every rank's sample count in one MAX all-reduce (the counts in per-rank
+        # slots, -1 elsewhere)
+        world, me = dist.get_world_size(process_group), dist.get_rank(process_group)
+        rng = torch.full((2 + world,), -1, dtype=torch.int64)
+        rng[0], rng[1], rng[2 + me] = (int(y.max()) if n else -1), (-int(y.min()) if n else 0), n
+        rng = rng.to(cdev)
         dist.all_reduce(rng, op=dist.ReduceOp.MAX, group=process_group)
-        dist.all_reduce(nn_, group=process_group)
-        ymax, ymin, n_all = int(rng[0]), -int(rng[1]), int(nn_[0])
+        r = rng.tolist()
+        ymax, ymin, n_all = r[0], -r[1], sum(r[2:])
         if n_all == 0:
             raise ValueError("the sharded multinomial fit got no samples on any rank")
         if ymin < 0:
@@ -296,16 +300,14 @@ class CP_logistic_regression():
             # collectives first, then the rank-local checks with a collective verdict: a failure on
             # one rank raises on every rank instead of leaving the others in a later all-reduce
             self._sync_class_set(process_group)
-            dev, Xd, yd, plan, cw, W = _engine.agree(process_group, prepare)
-            import torch.distributed as dist
-            Wt = torch.tensor([W], dtype=torch.float64, device=f"cuda:{dev}")
-            dist.all_reduce(Wt, group=process_group)
-            W = float(Wt.item())
+            (dev, Xd, yd, plan, cw, _), W = _engine.fit_start(process_group, prepare, lambda o: o[5],
+                                                              lambda o: o[3].num_params)
         arena = plan.pack(self.Bcp)
         w = self.weights.to(f"cuda:{dev}", torch.float32).contiguous()
         vcb = _Verbose() if verbose == 2 else None
         convergence_reached, _ = run_adam_fit(plan, Xd, yd, cw, W, arena, w, lambda_L2, max_iter, tol, patience,
-                                              hp, self.loss_running, verbose_cb=vcb, process_group=process_group)
+                                              hp, self.loss_running, verbose_cb=vcb, process_group=process_group,
+                                              arena_checked=True)
         plan.unpack_into(arena, self.Bcp)
         if (verbose is True) or (verbose >= 1):
             print('Convergence reached' if convergence_reached else

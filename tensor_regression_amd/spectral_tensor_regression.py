@@ -381,20 +381,21 @@ class CP_linear_regression():
             if verbose in (2, 3) and isinstance(Xd, HostStream):
                 raise NotImplementedError("verbose=2/3 (per-iteration y_hat variance) is not offered for a HostStream X")
             return Xd, yd, dev, self._get_plan(Xd, Xd.shape[0])
-        # under a process group a rank-local failure raises on every rank (_engine.agree)
-        X, y, dev, plan = prepare() if process_group is None else _engine.agree(process_group, prepare)
-        n_global = float(X.shape[0])
-        if process_group is not None:
-            import torch.distributed as dist
-            n_t = torch.tensor([X.shape[0]], dtype=torch.float64, device=f"cuda:{dev}")
-            dist.all_reduce(n_t, group=process_group)
-            n_global = float(n_t.item())
+        # under a process group one collective settles the start (_engine.fit_start): a rank-local
+        # failure raises on every rank, the arena sizes agree, and the global sample count
+        if process_group is None:
+            X, y, dev, plan = prepare()
+            n_global = float(X.shape[0])
+        else:
+            (X, y, dev, plan), n_global = _engine.fit_start(process_group, prepare, lambda o: o[0].shape[0],
+                                                            lambda o: o[3].num_params)
         norm = n_global * y.shape[1]
         arena = self._arena(plan)
         w = self._weights(dev)
         vcb = _VerbosePrinter(plan, X, y, w, norm) if verbose in (2, 3) else None
         convergence_reached, _ = run_adam_fit(plan, X, y, None, norm, arena, w, lambda_L2, max_iter, tol, patience,
-                                              hp, self.loss_running, verbose_cb=vcb, process_group=process_group)
+                                              hp, self.loss_running, verbose_cb=vcb, process_group=process_group,
+                                              arena_checked=True)
         plan.unpack_into(arena, self.Bcp_n, self.Bcp_c, self.bias)
         if plan.last_stop < 0:
             print('Loss is NaN. Stopping.')

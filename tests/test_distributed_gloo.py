@@ -359,3 +359,49 @@ def test_local_failure_raises_on_every_rank(tmp_path):
     assert r[0][1] == r[1][1] == ("after", 2.0)
     for k in range(2):
         assert r[k][2] == ("mnl", "HipLibraryError") and r[k][3] == ("lin", "HipLibraryError"), r[k]
+
+
+def _worker_fit_start(rank, world, port, out_path):
+    """_engine.fit_start: one MAX all-reduce settles a sharded fit's start — the normaliser is the
+    sum of every rank's value (negative values and an empty shard included), a failure on one rank
+    raises on every rank, and unequal arena sizes raise ValueError on every rank."""
+    from tensor_regression_amd import _engine
+    _init(rank, world, port)
+    res = []
+    norms = [7.0, -2.5, 0.0][:world]
+    out, tot = _engine.fit_start(dist.group.WORLD, lambda: ("ok", rank), lambda o: norms[rank], lambda o: 11)
+    res.append(("sum", out, tot))
+
+    def failing():
+        if rank == world - 1:
+            raise KeyError("last rank only")
+        return 1
+    try:
+        _engine.fit_start(dist.group.WORLD, failing, lambda o: 1.0, lambda o: 3)
+        res.append(("fail", "no error"))
+    except Exception as e:
+        res.append(("fail", type(e).__name__))
+    try:
+        _engine.fit_start(dist.group.WORLD, lambda: 0, lambda o: 1.0, lambda o: 10 + rank)
+        res.append(("size", "no error"))
+    except ValueError as e:
+        res.append(("size", "ValueError" if "disagree" in str(e) else str(e)))
+    t = torch.ones(1)
+    dist.all_reduce(t)
+    res.append(("after", float(t)))
+    with open(f"{out_path}.{rank}", "w") as f:
+        f.write(repr(res))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_fit_start_one_collective(tmp_path, world):
+    out = str(tmp_path / "fs")
+    mp.spawn(_worker_fit_start, args=(world, _free_port(), out), nprocs=world, join=True)
+    r = [eval(open(f"{out}.{k}").read()) for k in range(world)]
+    want = sum([7.0, -2.5, 0.0][:world])
+    for k in range(world):
+        assert r[k][0] == ("sum", ("ok", k), want), r[k]
+        assert r[k][1] == ("fail", "KeyError" if k == world - 1 else "RuntimeError"), r[k]
+        assert r[k][2] == ("size", "ValueError"), r[k]
+        assert r[k][3] == ("after", float(world)), r[k]

@@ -76,7 +76,9 @@ def _data(case):
 
 
 def _fit(case, X, y, init, seed, process_group=None):
-    """Fit through the production class; returns (loss_running, factors as numpy, plan describe)."""
+    """Fit through the production class; returns (loss_running, factors as numpy, plan describe).
+    The gradient arena of the first iteration, as the Adam step received it (after the all-reduce
+    on a process group), is recorded in _FIRST_GRAD."""
     import tensor_regression_amd as tra
     from tensor_regression_amd import spectral_tensor_regression as SP
     Xd, yd = X.to(DEV), y.to(DEV)
@@ -102,6 +104,33 @@ def _fit(case, X, y, init, seed, process_group=None):
                    process_group=process_group)
         facs = [a.detach().cpu().numpy() for a in list(m.Bcp_n) + list(m.Bcp_c)] + [m.bias.detach().cpu().numpy()]
     return list(m.loss_running), facs, m._plan.describe
+
+
+_FIRST_GRAD = {}
+
+
+def _record_first_grad():
+    """Wrap the engine so the first iteration's gradient arena is kept: after the sharded fit's
+    all-reduce (gradient_allreduce's callable), or after the local gradient without a group."""
+    from tensor_regression_amd import _engine
+    orig_ga, orig_lg = _engine.gradient_allreduce, _engine.loss_grad_any
+    _FIRST_GRAD.clear()
+
+    def ga(process_group, device_index):
+        fn = orig_ga(process_group, device_index)
+
+        def wrapped(g):
+            fn(g)
+            _FIRST_GRAD.setdefault("grad", g.detach().clone().cpu())
+        _FIRST_GRAD["allreduce"] = True
+        return wrapped
+
+    def lg(plan, X, target, class_weight, norm, arena, weights, grad, **kw):
+        orig_lg(plan, X, target, class_weight, norm, arena, weights, grad, **kw)
+        if not _FIRST_GRAD.get("allreduce"):
+            _FIRST_GRAD.setdefault("grad", grad.detach().clone().cpu())
+    _engine.gradient_allreduce, _engine.loss_grad_any = ga, lg
+    return lambda: (setattr(_engine, "gradient_allreduce", orig_ga), setattr(_engine, "loss_grad_any", orig_lg))
 
 
 def _in_turns(fn, rank, world):
@@ -130,17 +159,19 @@ def _worker(rank, world, port, out):
         X, y, split, init = _data(case)
         lo, hi = (0, split) if rank == 0 else (split, X.shape[0])
         orig = _engine.loss_grad_any
+        restore = _record_first_grad()
         if case.endswith("_turns"):
-            _engine.loss_grad_any = _in_turns(orig, rank, world)
+            _engine.loss_grad_any = _in_turns(_engine.loss_grad_any, rank, world)
         with warnings.catch_warnings(record=True) as w:
             warnings.simplefilter("always")
             try:
                 lr, facs, desc = _fit(case, X[lo:hi].contiguous(), y[lo:hi].contiguous(), init, seed=7 + 5 * rank,
                                       process_group=dist.group.WORLD)
             finally:
+                restore()
                 _engine.loss_grad_any = orig
         res[case] = {"loss_running": lr, "factors": [torch.from_numpy(np.ascontiguousarray(f)) for f in facs],
-                     "describe": desc, "warnings": [str(x.message) for x in w]}
+                     "describe": desc, "warnings": [str(x.message) for x in w], "grad0": _FIRST_GRAD["grad"]}
     torch.save(res, f"{out}.{rank}")
     dist.barrier()
     dist.destroy_process_group()
@@ -160,7 +191,12 @@ def world2(tmp_path_factory):
 
 def _single(case):
     X, y, split, init = _data(case)
-    return _fit(case, X, y, init, seed=7)
+    restore = _record_first_grad()
+    try:
+        out = _fit(case, X, y, init, seed=7)
+    finally:
+        restore()
+    return out + (_FIRST_GRAD["grad"],)
 
 
 @pytest.mark.parametrize("case", CASES)
@@ -186,8 +222,19 @@ def test_world2_fit_matches_single_process(world2, case, capsys):
         assert "recovered=2pass" not in r0["describe"], r0["describe"]
         assert not r0["warnings"] and not r1["warnings"], (r0["warnings"], r1["warnings"])
     # and equal to one process fitting the concatenated shards from the same initial point
-    lr, facs, _ = _single(case)
+    lr, facs, _, g0 = _single(case)
     assert len(r0["loss_running"]) == len(lr) == ITERS
+    # the all-reduced gradient arena of the first iteration (the data gradients, the bias entries and
+    # the data-loss slot, each normalised by the GLOBAL sample count or class-weight total) equals
+    # the single process's at the same point, element by element — Adam normalises each
+    # coordinate's step by its own scale, so a gradient summed once too often would not show in
+    # the trajectory (the multinomial ranks start from different local draws, synchronised to
+    # rank 0's before the first iteration; the single process starts from seed 7 = rank 0's)
+    assert torch.equal(r0["grad0"], r1["grad0"])
+    a, b = r0["grad0"].double().numpy(), g0.double().numpy()
+    assert a.shape == b.shape
+    scale = np.abs(b).max()
+    np.testing.assert_allclose(a, b, rtol=RTOL, atol=RTOL * 1e-2 * scale)
     np.testing.assert_allclose(r0["loss_running"], lr, rtol=RTOL)
     assert len(facs) == len(r0["factors"])
     for a, b in zip(r0["factors"], facs):

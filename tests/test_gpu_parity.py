@@ -203,6 +203,9 @@ def _multinomial_golden(name, kind="auto"):
         assert want in plan.describe, plan.describe
         if kind in ("noduo", "spi1"):
             assert " duo " not in plan.describe, plan.describe
+    if name.startswith("mnl_bsp") and kind in ("auto", "split"):
+        # full-mantissa X of magnitude 1e-3 / 2e-2 on the split body's own shapes
+        assert "form=bf16split" in plan.describe, plan.describe
     cw, W = mm._class_weights(np.array(m["class_weights"]), dev, yd)
     arena = plan.pack(mm.Bcp)
     grad = torch.zeros(plan.num_grads, device=DEV)
@@ -316,7 +319,9 @@ def test_multinomial_lbfgs_golden(name):
                                   m["lbfgs_kwargs"], dtype=torch.float64)
     ours, ref32, ref64 = (np.asarray(v, np.float64) for v in (mm.loss_running, d["loss_running"], r64["loss_running"]))
     assert abs(ours[0] - ref32[0]) <= RTOL * abs(ref32[0])
-    spread = np.abs(ref32 - ref64).max()
+    # per step: the reference's largest fp32-vs-fp64 gap UP TO that step (x2), so the early steps,
+    # where the two reference runs barely differ, keep a tight bar
+    spread = np.maximum.accumulate(np.abs(ref32 - ref64))
     ok = (np.abs(ours - ref32) <= RTOL * np.abs(ref32)) | (np.abs(ours - ref64) <= 2 * spread + RTOL * np.abs(ref64))
     assert ok.all(), (ours, ref32, ref64)
     closure_parity(final=True)  # the kernels at the point the GPU trajectory reached
@@ -500,21 +505,16 @@ def test_multinomial_sweep_vs_oracle(shape, C, rank, kind):
         _multinomial_sweep(shape, C, rank)
 
 
-@pytest.mark.parametrize("ring", ["auto", "2"])
 @pytest.mark.parametrize("shape,C,rank", WIDE_SHAPES)
-def test_multinomial_wide_split_body_selected(shape, C, rank, ring, monkeypatch):
+def test_multinomial_wide_split_body_selected(shape, C, rank, monkeypatch):
     """(32 NW, 64) and (16 NW, 128) samples with R <= 8 take the split body with NW waves per
     workgroup by default (describe 'form=bf16split waves=NW'), with a ring of three samples at
-    NW = 5, 6 (nbuf=3; TR_DUO_RING=2 keeps two); the results are the sweep's.  A padded sample
-    filling less than a third of its padded shape runs the two-pass kernels by default and the
-    split body with TR_DUO_ANYFILL=1."""
-    monkeypatch.delenv("TR_DUO_RING", raising=False)
+    NW = 5, 6 (nbuf=3); the results are the sweep's.  A padded sample filling less than a third
+    of its padded shape runs the two-pass kernels by default and the split body with
+    TR_DUO_ANYFILL=1."""
     monkeypatch.delenv("TR_DUO_ANYFILL", raising=False)
-    if ring == "2":
-        monkeypatch.setenv("TR_DUO_RING", "2")
     nw = _split_waves(shape[1], shape[2])
     jt = _split_jt(shape[2])
-    padded = shape[1] != (32 if jt == 64 else 16) * nw or shape[2] != jt
     if 3 * shape[1] * shape[2] < (32 if jt == 64 else 16) * nw * jt:
         with path("auto"):
             desc = _multinomial_sweep(shape, C, rank)
@@ -522,8 +522,9 @@ def test_multinomial_wide_split_body_selected(shape, C, rank, ring, monkeypatch)
         monkeypatch.setenv("TR_DUO_ANYFILL", "1")
     with path("auto"):
         desc = _multinomial_sweep(shape, C, rank)
-    # (the padded (16 NW, 128) body with a ring of three spills at NW = 6: the plan takes two slots)
-    nbuf = 3 if nw in (5, 6) and ring == "auto" and not (padded and jt == 128) else 2
+    # (round 5's padded (16 NW, 128) body with a ring of three spilled at NW = 6 and took two slots;
+    # with three bf16 X pieces it holds 243 VGPRs and no scratch)
+    nbuf = 3 if nw in (5, 6) else 2
     assert "form=bf16split" in desc and f"waves={nw} wg/cu={8 // nw} nbuf={nbuf} " in desc, desc
 
 
@@ -558,6 +559,64 @@ def _multinomial_sweep(shape, C, rank):
     S = plan.forward(Xd, arena, mm.weights)
     np.testing.assert_allclose(S.cpu().numpy(), ref["probs"], rtol=RTOL, atol=1e-6)
     return plan.describe
+
+
+# the split body's shapes (one per wave count and ring depth, padded rows and widths) plus config 3's
+# sample at rank 3 (the split body by default) and at rank 8 with TR_DUO_SPLIT=1
+SPLIT_SCALE_SHAPES = [((300, 64, 64), 10, 8, "auto"), ((200, 96, 64), 7, 3, "auto"), ((90, 160, 64), 4, 8, "auto"),
+                      ((60, 224, 64), 3, 6, "auto"), ((150, 256, 64), 16, 5, "auto"),
+                      ((120, 96, 128), 6, 7, "auto"), ((80, 128, 128), 10, 8, "auto"),
+                      ((300, 100, 64), 10, 8, "auto"), ((200, 128, 48), 10, 8, "auto"), ((80, 70, 128), 4, 8, "auto"),
+                      ((256, 128, 64), 10, 3, "auto"), ((256, 128, 64), 10, 8, "split")]
+
+
+@pytest.mark.parametrize("xscale", [1e-4, 1e-2, 1e4, 3e7])
+@pytest.mark.parametrize("shape,C,rank,kind", SPLIT_SCALE_SHAPES)
+def test_multinomial_split_body_x_scale(shape, C, rank, kind, xscale):
+    """The bf16-split body (k_mnl_bsp) at data scales far from 1: X = N(0, 1) * xscale with the
+    feature factors scaled by xscale^-1/2 each (the logits stay O(1); plain factors, since softplus
+    is not scale-equivariant; no L2 term, so every gradient is the data term).  X goes to the MFMAs
+    as three exact bf16 pieces, so the representation loses nothing at any scale; round 5's f16
+    second piece was 2e-4 off at xscale 1e-4 and overflowed to inf at 3e7.  Bars, every gradient
+    and the loss: finite; within 1e-5 (normwise) of the reference's op sequence in fp32 (the
+    oracle); and no further from the fp64 closed form than twice the oracle's own fp32 error
+    + 1e-7 (normwise)."""
+    from oracle import cp_oracle
+    from tensor_regression_amd import CP_logistic_regression
+    g = torch.Generator().manual_seed(hash((shape, C, rank, kind)) % 2**31)
+    X = torch.randn(*shape, generator=g) * xscale
+    y = torch.randint(0, C, (shape[0],), generator=g)
+    y[:C] = torch.arange(C)
+    P = int(np.prod(shape[1:]))
+    sc = 0.3 * min(1.0, (2048.0 / P) ** 0.5)
+    fs = xscale ** -0.5
+    Bcp0 = [torch.randn(shape[1], rank, generator=g) * sc * fs, torch.randn(shape[2], rank, generator=g) * sc * fs,
+            torch.randn(C, rank, generator=g) * sc]
+    cw = (torch.rand(C, generator=g) + 0.5).numpy()
+    nn = [False, False, False]
+    ref32 = cp_oracle.mnl_loss_grad(X, y, Bcp0, np.ones(rank), nn, cw, 0.0)
+    ref64 = cp_oracle.closed_form_mnl(X.double().numpy(), y.numpy(), [b.double().numpy() for b in Bcp0],
+                                      np.ones(rank), nn, cw, 0.0)
+    with path(kind):
+        mm = CP_logistic_regression(X.numpy(), y.numpy(), rank=rank, non_negative=nn, device=DEV,
+                                    Bcp_init=[b.to(DEV) for b in Bcp0])
+        dev, Xd, yd = mm._device_data()
+        plan = mm._get_plan(Xd, shape[0])
+        assert "form=bf16split" in plan.describe, plan.describe
+        cwd, W = mm._class_weights(cw, dev, yd)
+        arena = plan.pack(mm.Bcp)
+        grad = torch.zeros(plan.num_grads, device=DEV)
+        gtot = torch.zeros(plan.num_params, device=DEV)
+        loss = torch.zeros(1, device=DEV)
+        plan.loss_grad(Xd, yd, cwd, W, arena, mm.weights, grad)
+        plan.finalize_grad(arena, grad, 0.0, gtot, loss)
+        ours = [t.cpu().numpy() for t in plan.factor_views(gtot)]
+    assert np.isfinite(loss.item()) and all(np.isfinite(o).all() for o in ours)
+    assert abs(loss.item() - ref32["loss"]) <= RTOL * abs(ref32["loss"])
+    for f, (o, r32, r64) in enumerate(zip(ours, ref32["grads"], ref64["grads"])):
+        e32, e_ref, e_ours = normwise_rel(o, r32), normwise_rel(r32, r64), normwise_rel(o, r64)
+        assert e32 <= RTOL, (f, e32)
+        assert e_ours <= 2 * e_ref + 1e-7, (f, e_ours, e_ref)
 
 
 @pytest.mark.parametrize("shape", [(3000, 64, 32), (700, 64, 64, 32)])

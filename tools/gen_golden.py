@@ -130,9 +130,17 @@ def linear_lbfgs_case(name, seed, shape, rank, lam, iters, lbfgs_kwargs, logging
 
 
 def mnl_case(name, seed, shape, n_classes, rank, non_negative, class_w, lam, adam_kwargs, iters, tol=0.0,
-             patience=10):
+             patience=10, x_scale=None):
+    """x_scale: X = N(0, 1) * x_scale in float32 (full mantissa, stored as X_f32) instead of the exact
+    int8 / 8 X: every bf16 piece of a split kernel's X representation then carries data, at a
+    magnitude far from 1 (the f16 second piece of round 5's split body lost precision below
+    |x| = 2^-5)."""
     rng = np.random.default_rng(seed)
-    Xq, X = exact_X(rng, shape)
+    if x_scale is None:
+        Xq, X = exact_X(rng, shape)
+    else:
+        Xq = None
+        X = torch.tensor((rng.standard_normal(shape) * x_scale).astype(np.float32))
     y = rng.integers(0, n_classes, size=shape[0])
     y[:n_classes] = np.arange(n_classes)  # every class present (n_classes = len(unique(y)))
     torch.manual_seed(seed)
@@ -156,7 +164,8 @@ def mnl_case(name, seed, shape, n_classes, rank, non_negative, class_w, lam, ada
                 adam_kwargs=adam_kwargs, max_iter=iters, tol=tol, patience=patience,
                 softplus_kwargs=m.softplus_kwargs, factor_shapes=[list(a.shape) for a in Bcp0],
                 torch=torch.__version__)
-    save(name, X_q=Xq, y=y.astype(np.int64), Bcp0=np.concatenate([a.reshape(-1) for a in Bcp0]),
+    xarr = dict(X_q=Xq) if Xq is not None else dict(X_f32=X.numpy())
+    save(name, **xarr, y=y.astype(np.int64), Bcp0=np.concatenate([a.reshape(-1) for a in Bcp0]),
          probs0=S.detach().numpy(), loss0=np.float64(loss.item()),
          grads0=np.concatenate([g.reshape(-1) for g in grads]),
          loss_running=np.array(m.loss_running, dtype=np.float64),
@@ -480,6 +489,12 @@ def main():
     mnl_case("mnl_duo_shape", 42, (96, 128, 64), 10, 8, [False, False, False], [1.0] * 10, 0.01, adam, 40)
     mnl_case("mnl_duo_t", 43, (80, 64, 128), 6, 7, [True, False, True], [0.5, 2.0, 1.0, 1.5, 0.8, 1.2], 0.02,
              {'lr': 0.01, 'amsgrad': True}, 40)
+    # full-mantissa X of small magnitude on the split body's shapes ((64, 64) rank 3: two 32-row waves;
+    # (64, 128) rank 5: four 16-row waves), fitted by the reference's own fit_Adam
+    mnl_case("mnl_bsp_f32x_small", 48, (32, 64, 64), 4, 3, [False, False, False], [1.0, 0.5, 2.0, 1.5], 0.01,
+             {'lr': 0.01}, 40, x_scale=1e-3)
+    mnl_case("mnl_bsp_f32x_j128", 49, (16, 64, 128), 6, 5, [False, False, False], [1.0] * 6, 0.01,
+             {'lr': 0.01, 'amsgrad': True}, 30, x_scale=2e-2)
     init_case("init_rng")
     spectral_case("spec_basic", 31, (64, 12, 9), 3, 2, 2, 1, False, 0.01, adam, 50)
     spectral_case("spec_nonneg_amsgrad_wd", 32, (80, 16, 17), 2, 3, 2, 2, [True, False, True], 0.02,

@@ -22,9 +22,6 @@
 #ifndef TR_UPD_PROFILE
 #define TR_UPD_PROFILE 0
 #endif
-#ifndef TR_UPD_TRIP
-#define TR_UPD_TRIP 2
-#endif
 #include "tr_update.hip"  // the library kernel (v5)
 
 #define CK(x)                                                                       \
