@@ -517,10 +517,6 @@ def main():
         plan.set_timing(True, kinds=None if args.time_all_kernels else ["stream_fused", "stream_rows", "stream_cols"],
                         every=max(1, args.timing_every))
 
-    def barrier():
-        if pg is not None:
-            torch.distributed.barrier()
-
     comm = None
     if pg is not None:  # (world 1 too with TR_BENCH_FORCE_PG=1: the RCCL path on one GPU)
         from tensor_regression_amd import _engine
@@ -529,6 +525,15 @@ def main():
             comm.set_timing(args.allreduce_sample_every)
         else:
             comm = None
+
+    def barrier():
+        # every rank past this point once all have reached it: on RCCL a one-element ncclAllReduce
+        # on the compute stream + device sync (RcclAllReduce.barrier; dist.barrier() through
+        # ProcessGroupNCCL cost ~55 us per call at world 1, tools/pg_account.py)
+        if comm is not None:
+            comm.barrier()
+        elif pg is not None:
+            torch.distributed.barrier()
 
     _ph("set_timing")
     barrier()

@@ -550,14 +550,18 @@ def fit_start(process_group, fn, norm_of, size_of):
         out = fn()
     except Exception as e:  # re-raised below, after the other ranks have been told
         err = e
-    v = torch.full((3 + world,), float("-inf"), dtype=torch.float64)
+    v = [float("-inf")] * (3 + world)
     v[0] = 0.0 if err is None else 1.0
     if err is None:
         size = float(size_of(out))
         v[1], v[2], v[3 + me] = size, -size, float(norm_of(out))
-    v = v.to(collective_device(process_group))
-    dist.all_reduce(v, op=dist.ReduceOp.MAX, group=process_group)
-    r = v.tolist()
+    comm = direct_comm(process_group, None)
+    if comm is not None:  # RCCL: ncclAllReduce on the compute stream (RcclAllReduce.max_f64)
+        r = comm.max_f64(v)
+    else:
+        t = torch.tensor(v, dtype=torch.float64, device=collective_device(process_group))
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=process_group)
+        r = t.tolist()
     if err is not None:
         raise err
     if r[0] > 0:
@@ -596,6 +600,10 @@ def sync_replicas(arena, process_group, checked=False):
     import torch.distributed as dist
     if not checked:
         check_uniform(arena.numel(), process_group, "the parameter arena size", arena.device)
+    comm = direct_comm(process_group, arena.device.index if arena.is_cuda else None)
+    if comm is not None:  # RCCL: ncclBroadcast on the compute stream
+        comm.broadcast(arena, root=0)
+        return
     src = dist.get_global_rank(process_group, 0) if process_group is not None else 0
     dist.broadcast(arena, src=src, group=process_group)
 
@@ -653,14 +661,16 @@ def _rccl_lib():
     lib.ncclCommInitRank.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, _UniqueId, ctypes.c_int]
     lib.ncclAllReduce.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
                                   ctypes.c_void_p, ctypes.c_void_p]
+    lib.ncclBroadcast.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
+                                  ctypes.c_void_p, ctypes.c_void_p]
     lib.ncclCommDestroy.argtypes = [ctypes.c_void_p]
     lib.ncclGetErrorString.restype = ctypes.c_char_p
     lib.ncclGetErrorString.argtypes = [ctypes.c_int]
     lib.ncclCommGetAsyncError.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
     lib.ncclCommAbort.argtypes = [ctypes.c_void_p]
     lib.ncclCommCount.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
-    for fn in ("ncclGetUniqueId", "ncclCommInitRank", "ncclAllReduce", "ncclCommDestroy", "ncclCommGetAsyncError",
-               "ncclCommAbort", "ncclCommCount"):
+    for fn in ("ncclGetUniqueId", "ncclCommInitRank", "ncclAllReduce", "ncclBroadcast", "ncclCommDestroy",
+               "ncclCommGetAsyncError", "ncclCommAbort", "ncclCommCount"):
         getattr(lib, fn).restype = ctypes.c_int
     return lib
 
@@ -750,6 +760,38 @@ class RcclAllReduce:
             ev.record(torch.cuda.current_stream(self.dev))
             self._pending.append(ev)
 
+    def max_f64(self, values):
+        """MAX all-reduce of a short host list of floats over the ranks (ncclAllReduce, ncclMax, on
+        the compute stream) and its result back on the host: the host-logic collective of a
+        sharded fit's start (fit_start), without torch's collective stream and its event joins
+        (≈ 80 µs per call at world 1 through ProcessGroupNCCL, tools/pg_account.py)."""
+        dev = torch.device("cuda", self.dev)
+        buf = getattr(self, "_f64_buf", None)
+        if buf is None or buf.numel() != len(values):
+            buf = torch.empty(len(values), dtype=torch.float64, device=dev)
+            self._f64_host = torch.empty(len(values), dtype=torch.float64, pin_memory=True)
+            self._f64_buf = buf
+        self._f64_host.copy_(torch.tensor(values, dtype=torch.float64))
+        buf.copy_(self._f64_host, non_blocking=True)
+        p = ctypes.c_void_p(buf.data_ptr())
+        self._check(self.lib.ncclAllReduce(p, p, buf.numel(), 8, 2, self.comm, stream_handle(self.dev)),
+                    "ncclAllReduce(max)")  # ncclFloat64, ncclMax
+        self._f64_host.copy_(buf, non_blocking=True)
+        torch.cuda.current_stream(self.dev).synchronize()
+        return self._f64_host.tolist()
+
+    def broadcast(self, t, root=0):
+        """ncclBroadcast of a device tensor from communicator rank `root`, on the compute stream."""
+        dt = {torch.float32: 7, torch.float64: 8}[t.dtype]
+        p = ctypes.c_void_p(t.data_ptr())
+        self._check(self.lib.ncclBroadcast(p, p, t.numel(), dt, int(root), self.comm, stream_handle(self.dev)),
+                    "ncclBroadcast")
+
+    def barrier(self):
+        """Every rank past this point once all have reached it: a one-element all-reduce on the
+        compute stream, then a device synchronisation (bench.py's timed-region bracket)."""
+        self.max_f64([0.0])
+
     def wait(self, timeout=None):
         """Block until the work queued on the current stream (this rank's all-reduces included) has
         finished, polling the communicator: an asynchronous RCCL error, or `timeout` seconds
@@ -823,21 +865,32 @@ def _destroy_rccl_comms():
     _rccl_comms.clear()
 
 
+def direct_comm(process_group, device_index):
+    """The process's RcclAllReduce communicator for an NCCL (= RCCL) group on `device_index` (the
+    current device when None), built on first use (collective: every rank of the group calls it
+    at the same point); None for other backends or with TR_RCCL_DIRECT=0."""
+    import torch.distributed as dist
+    if not (_RCCL_DIRECT and dist.get_backend(process_group) == "nccl"):
+        return None
+    if device_index is None:
+        device_index = torch.cuda.current_device()
+    key = (tuple(dist.get_process_group_ranks(process_group)), int(device_index))
+    comm = _rccl_comms.get(key)
+    if comm is None:
+        comm = RcclAllReduce(process_group, device_index)
+        if not _rccl_comms:
+            atexit.register(_destroy_rccl_comms)  # LIFO: before torch's and HIP's teardown
+        _rccl_comms[key] = comm
+    return comm
+
+
 def gradient_allreduce(process_group, device_index):
     """The per-iteration sum all-reduce of the gradient arena for `process_group`: ncclAllReduce on
     the compute stream (RcclAllReduce) for an NCCL group, torch.distributed.all_reduce otherwise
     (gloo; or TR_RCCL_DIRECT=0).  Collective: every rank of the group calls it at the same point."""
     import torch.distributed as dist
-    if _RCCL_DIRECT and dist.get_backend(process_group) == "nccl":
-        if device_index is None:
-            device_index = torch.cuda.current_device()
-        key = (tuple(dist.get_process_group_ranks(process_group)), int(device_index))
-        comm = _rccl_comms.get(key)
-        if comm is None:
-            comm = RcclAllReduce(process_group, device_index)
-            if not _rccl_comms:
-                atexit.register(_destroy_rccl_comms)  # LIFO: before torch's and HIP's teardown
-            _rccl_comms[key] = comm
+    comm = direct_comm(process_group, device_index)
+    if comm is not None:
         return comm
 
     def allreduce(g):

@@ -57,6 +57,10 @@
 //    lanes, lanes past the Dt tail rows masked by an out-of-range offset) right after the wave's
 //    pieces of the tiles that hold its tail rows (their 128-B lines are then on their way into L2);
 //  - the epilogue's table reads carry no per-element lane masks (see tab8).
+#ifndef TR_SLICE_ACC
+#define TR_SLICE_ACC 0  // EXPERIMENT: 1 gradient products into a zero accumulator per sample, added by VALU;
+                        // 2 the forward's per k step as well
+#endif
 #ifndef TR_SLICE_PROFILE
 #define TR_SLICE_PROFILE 0  // profiling build: per-phase cycle counts of wave 0 of workgroups 0..255
 #endif
@@ -239,6 +243,10 @@ __device__ __forceinline__ sl_f4 sl_mfma_lp(const sl_u4 (&a)[3], const sl_u4 (&b
 // packed (Rn <= 8) / not; 3 / 4 the same with the three-piece X
 #define SL_LP(SP) ((SP) == 1 || (SP) == 3)
 #define SL_XP(SP) ((SP) >= 3 ? 3 : 2)
+#ifndef TR_SLICE_FWD3
+#define TR_SLICE_FWD3 0  // EXPERIMENT: the forward's X in three pieces whatever SP says
+#endif
+#define SL_XPF(SP) (TR_SLICE_FWD3 ? 3 : SL_XP(SP))
 template <int CTRL>
 __device__ __forceinline__ float sl_dpp(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
@@ -611,19 +619,32 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
           // tile q holds elements 4 (q & 1) .. +3 of k step q / 2: VGPRs 2 (q & 1), 2 (q & 1) + 1
 #pragma unroll
           for (int mm = 0; mm < 2; ++mm) {
-            sl_splitx_m<SL_XP(SP)>(xa[2 * mm].x, xa[2 * mm + 1].x, xf[0], 2 * (q & 1) + mm);
-            sl_splitx_m<SL_XP(SP)>(xa[2 * mm].y, xa[2 * mm + 1].y, xf[1], 2 * (q & 1) + mm);
+            sl_splitx_m<SL_XPF(SP)>(xa[2 * mm].x, xa[2 * mm + 1].x, xf[0], 2 * (q & 1) + mm);
+            sl_splitx_m<SL_XPF(SP)>(xa[2 * mm].y, xa[2 * mm + 1].y, xf[1], 2 * (q & 1) + mm);
           }
           if ((q & 1) && !(TR_SLICE_SKIP & 2)) {
             const int S = q >> 1;
-            T00 = sl_mfma6<SL_XP(SP)>(xf[0], bs[S], T00);
-            T01 = sl_mfma6<SL_XP(SP)>(xf[1], bs[S], T01);
-            if constexpr (SL_LP(SP)) {
-              T10 = sl_mfma_lp<SL_XP(SP)>(xf[0], bl[S], T10);
-              T11 = sl_mfma_lp<SL_XP(SP)>(xf[1], bl[S], T11);
+            if (TR_SLICE_ACC & 2) {
+              const sl_f4 z = {0.f, 0.f, 0.f, 0.f};
+              T00 += sl_mfma6<SL_XPF(SP)>(xf[0], bs[S], z);
+              T01 += sl_mfma6<SL_XPF(SP)>(xf[1], bs[S], z);
+              if constexpr (SL_LP(SP)) {
+                T10 += sl_mfma_lp<SL_XPF(SP)>(xf[0], bl[S], z);
+                T11 += sl_mfma_lp<SL_XPF(SP)>(xf[1], bl[S], z);
+              } else {
+                T10 += sl_mfma6<SL_XPF(SP)>(xf[0], bl[S], z);
+                T11 += sl_mfma6<SL_XPF(SP)>(xf[1], bl[S], z);
+              }
             } else {
-              T10 = sl_mfma6<SL_XP(SP)>(xf[0], bl[S], T10);
-              T11 = sl_mfma6<SL_XP(SP)>(xf[1], bl[S], T11);
+            T00 = sl_mfma6<SL_XPF(SP)>(xf[0], bs[S], T00);
+            T01 = sl_mfma6<SL_XPF(SP)>(xf[1], bs[S], T01);
+            if constexpr (SL_LP(SP)) {
+              T10 = sl_mfma_lp<SL_XPF(SP)>(xf[0], bl[S], T10);
+              T11 = sl_mfma_lp<SL_XPF(SP)>(xf[1], bl[S], T11);
+            } else {
+              T10 = sl_mfma6<SL_XPF(SP)>(xf[0], bl[S], T10);
+              T11 = sl_mfma6<SL_XPF(SP)>(xf[1], bl[S], T11);
+            }
             }
           }
         }
@@ -675,14 +696,14 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
         for (int m = 0; m < 4; ++m) {
           const float x0 = i < Dt ? sTail[i * TR + 8 * m + gq] : 0.f;
           const float x1 = i < Dt ? sTail[i * TR + 8 * m + 4 + gq] : 0.f;
-          sl_splitx_m<SL_XP(SP)>(x0, x1, tf, m);
+          sl_splitx_m<SL_XPF(SP)>(x0, x1, tf, m);
         }
         auto tail_step = [&](const sl_u4(&b_s)[3], const sl_u4(&b_l)[NL]) {
-          Tts = sl_mfma6<SL_XP(SP)>(tf, b_s, Tts);
+          Tts = sl_mfma6<SL_XPF(SP)>(tf, b_s, Tts);
           if constexpr (SL_LP(SP))
-            Ttl = sl_mfma_lp<SL_XP(SP)>(tf, b_l, Ttl);
+            Ttl = sl_mfma_lp<SL_XPF(SP)>(tf, b_l, Ttl);
           else
-            Ttl = sl_mfma6<SL_XP(SP)>(tf, b_l, Ttl);
+            Ttl = sl_mfma6<SL_XPF(SP)>(tf, b_l, Ttl);
         };
         switch (p) {
           case 0: tail_step(bs[0], bl[0]); break;
@@ -947,16 +968,24 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
               }
               if (q + 1 < ntl) dma_piece(nn, q + 1, 0);
             }
-            if (!(TR_SLICE_SKIP & 4)) gacc[q][0] = sl_mfma6<SL_XP(SP)>(af, ds, gacc[q][0]);
+            if (!(TR_SLICE_SKIP & 4)) {
+              if (TR_SLICE_ACC & 1)
+                gacc[q][0] += sl_mfma6<SL_XP(SP)>(af, ds, sl_f4{0.f, 0.f, 0.f, 0.f});
+              else
+                gacc[q][0] = sl_mfma6<SL_XP(SP)>(af, ds, gacc[q][0]);
+            }
             if (has_next && q + 1 < ntl) {
               dma_piece(nn, q + 1, 1);
               if (TAIL_LAST && Dt > 0 && q + 1 == qt) dma_tail(nn);
             }
             if (!(TR_SLICE_SKIP & 4)) {
+              const sl_f4 c1 = (TR_SLICE_ACC & 1) ? sl_f4{0.f, 0.f, 0.f, 0.f} : gacc[q][1];
+              sl_f4 r1;
               if constexpr (SL_LP(SP))
-                gacc[q][1] = sl_mfma_lp<SL_XP(SP)>(af, dl, gacc[q][1]);
+                r1 = sl_mfma_lp<SL_XP(SP)>(af, dl, c1);
               else
-                gacc[q][1] = sl_mfma6<SL_XP(SP)>(af, dl, gacc[q][1]);
+                r1 = sl_mfma6<SL_XP(SP)>(af, dl, c1);
+              gacc[q][1] = (TR_SLICE_ACC & 1) ? gacc[q][1] + r1 : r1;
             }
           }
           if (Dt > 0 && q / TQ == p) {

@@ -9,17 +9,20 @@ never get materialised:
 * `windowed_view(X_untiled, y, win_range)` — every usable window, in `usable_idx` order, as one
   overlapping strided view (N, L, *F) with stride F along the sample axis.  X stays T x F in
   HBM; each kernel reads sample n at X + n*F (`tr_plan_set_x_stride`).
-* `WindowedDataset` — the reference's indexing surface (`usable_idx`, `ds[idx]`) over that view.
+* `WindowedDataset` — the reference's `torch.utils.data.Dataset` (`usable_idx`, `ds[idx]`,
+  `len(ds)` = series length, the `transform` / `target_transform` arguments) over that view.
+* `make_WindowedDataloader` — the reference's random-minibatch loader over the usable windows
+  (util.py:100-114), returning (dataloader, dataset, sampler) with `dataloader.sample_shape`.
 * `HostStream` — an X kept in pinned host memory and streamed through two device buffers per
   iteration, for an X larger than the HBM one wants to spend.
 
-The reference's general helpers (`set_device`, `squeeze_integers`, `make_WindowedDataloader`'s
-random minibatching) are not on the fit path and are not provided.
+The reference's general helpers (`set_device`, `squeeze_integers`) are not on the fit path and
+are not provided.
 """
 import numpy as np
 import torch
 
-__all__ = ["windowed_view", "WindowedDataset", "HostStream"]
+__all__ = ["windowed_view", "WindowedDataset", "make_WindowedDataloader", "HostStream"]
 
 
 def _usable_idx(T, win_range):
@@ -54,32 +57,57 @@ def windowed_view(X_untiled, y, win_range):
     return Xw, yw
 
 
-class WindowedDataset:
-    """Indexable windows of an untiled series with the reference's sample numbering (util.py:67-98).
+class WindowedDataset(torch.utils.data.Dataset):
+    """Indexable windows of an untiled series with the reference's sample numbering (util.py:67-98),
+    a `torch.utils.data.Dataset` like the reference's.
 
     `ds[idx]` for idx in `ds.usable_idx` returns (window, target) as views into the strided
-    `ds.windows` / gathered `ds.targets` (the tensors a fit takes directly).  Deviation: an idx
-    outside `usable_idx` raises IndexError, where the reference returns a truncated window.
-    `len(ds)` is the number of usable windows (the reference reports the series length).
+    `ds.windows` / gathered `ds.targets` (the tensors a fit takes directly).  `len(ds)` is the
+    series length, as in the reference (util.py:78-79; `ds.n_windows` is the number of usable
+    windows).  `transform` / `target_transform` are accepted and, as in the reference (which
+    stores neither), not applied.  Deviation: an idx outside `usable_idx` raises IndexError, where
+    the reference returns a truncated (or, for a negative start, wrapped) window.
     """
 
-    def __init__(self, X_untiled, y_input, win_range):
+    def __init__(self, X_untiled, y_input, win_range, transform=None, target_transform=None):
         if len(X_untiled) != len(y_input):
-            raise ValueError(f"X_untiled and y_input need the same length along dim 0, got "
-                             f"{len(X_untiled)} and {len(y_input)}")
+            # (the reference's message: util.py:75-76)
+            raise ValueError('RH: X and y must have same first dimension shape')
+        self.X_untiled = X_untiled
+        self.y_input = y_input
         self.win_range = (int(win_range[0]), int(win_range[1]))
+        self.n_samples = int(len(y_input))
         self.windows, self.targets = windowed_view(X_untiled, y_input, self.win_range)
         self.usable_idx = _usable_idx(len(X_untiled), self.win_range)
 
-    def __len__(self):
+    @property
+    def n_windows(self):
         return int(self.windows.shape[0])
+
+    def __len__(self):
+        return self.n_samples
 
     def __getitem__(self, idx):
         n = int(idx) + self.win_range[0]
-        if not 0 <= n < len(self):
+        if not 0 <= n < self.n_windows:
             raise IndexError(f"window index {int(idx)} is outside usable_idx "
                              f"[{int(self.usable_idx[0])}, {int(self.usable_idx[-1])}]")
         return self.windows[n], self.targets[n]
+
+
+def make_WindowedDataloader(X, y, win_range=[-10, 10], batch_size=64, drop_last=True, **kwargs_dataloader):
+    """The reference's minibatch loader over the usable windows (util.py:100-114): a
+    `WindowedDataset`, a `SubsetRandomSampler` over its `usable_idx` and a `DataLoader` with the
+    given batch size, `drop_last` and extra DataLoader arguments; `dataloader.sample_shape` =
+    [batch_size] + one window's shape.  Returns (dataloader, dataset, sampler).  Each batch stacks
+    its windows (the reference's host-side path); a fit over ALL windows takes
+    `dataset.windows` / `dataset.targets` instead, which are never materialised."""
+    dataset = WindowedDataset(X, y, win_range)
+    sampler = torch.utils.data.SubsetRandomSampler(dataset.usable_idx, generator=None)
+    dataloader = torch.utils.data.DataLoader(dataset, batch_size=batch_size, drop_last=drop_last, sampler=sampler,
+                                             **kwargs_dataloader)
+    dataloader.sample_shape = [dataloader.batch_size] + list(dataset[-win_range[0]][0].shape)
+    return dataloader, dataset, sampler
 
 
 class HostStream:

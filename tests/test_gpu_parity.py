@@ -204,8 +204,10 @@ def _multinomial_golden(name, kind="auto"):
         if kind in ("noduo", "spi1"):
             assert " duo " not in plan.describe, plan.describe
     if name.startswith("mnl_bsp") and kind in ("auto", "split"):
-        # full-mantissa X of magnitude 1e-3 / 2e-2 on the split body's own shapes
-        assert "form=bf16split" in plan.describe, plan.describe
+        # full-mantissa X of magnitude 1e-3 / 2e-2 on the duo family's shapes: the split body (and at
+        # the 32 KiB (64, 128) sample of rank 5 the rank-block body by default)
+        want = "form=bf16split" if kind == "split" or m["rank"] <= 4 else "form=rankblock"
+        assert want in plan.describe, plan.describe
     cw, W = mm._class_weights(np.array(m["class_weights"]), dev, yd)
     arena = plan.pack(mm.Bcp)
     grad = torch.zeros(plan.num_grads, device=DEV)
@@ -570,21 +572,28 @@ SPLIT_SCALE_SHAPES = [((300, 64, 64), 10, 8, "auto"), ((200, 96, 64), 7, 3, "aut
                       ((256, 128, 64), 10, 3, "auto"), ((256, 128, 64), 10, 8, "split")]
 
 
-@pytest.mark.parametrize("xscale", [1e-4, 1e-2, 1e4, 3e7])
+@pytest.mark.parametrize("xscale", [1e-4, 1e-2, 1.0, 1e4, 3e7, "mixed"])
 @pytest.mark.parametrize("shape,C,rank,kind", SPLIT_SCALE_SHAPES)
 def test_multinomial_split_body_x_scale(shape, C, rank, kind, xscale):
     """The bf16-split body (k_mnl_bsp) at data scales far from 1: X = N(0, 1) * xscale with the
     feature factors scaled by xscale^-1/2 each (the logits stay O(1); plain factors, since softplus
-    is not scale-equivariant; no L2 term, so every gradient is the data term).  X goes to the MFMAs
-    as three exact bf16 pieces, so the representation loses nothing at any scale; round 5's f16
-    second piece was 2e-4 off at xscale 1e-4 and overflowed to inf at 3e7.  Bars, every gradient
-    and the loss: finite; within 1e-5 (normwise) of the reference's op sequence in fp32 (the
-    oracle); and no further from the fp64 closed form than twice the oracle's own fp32 error
-    + 1e-7 (normwise)."""
+    is not scale-equivariant; no L2 term, so every gradient is the data term); "mixed": every
+    sample at its own scale 10^U(-4, 4), so one launch runs both X forms.  A wave takes the fast
+    form (a bf16 piece and an f16 residual) where its largest |x| lies in [2^-5, 2^24) and the
+    exact three-piece bf16 form elsewhere (xscale 1e-4 and 3e7 here, 1e-2 in part); round 5's
+    single form was 2e-4 off at xscale 1e-4 and overflowed to inf at 3e7.  Bars, every gradient and
+    the loss: finite; within 1e-5 (normwise) of the reference's op sequence in fp32 (the oracle);
+    and no further from the fp64 closed form than twice the oracle's own fp32 error + 1e-7
+    (normwise)."""
     from oracle import cp_oracle
     from tensor_regression_amd import CP_logistic_regression
     g = torch.Generator().manual_seed(hash((shape, C, rank, kind)) % 2**31)
-    X = torch.randn(*shape, generator=g) * xscale
+    X = torch.randn(*shape, generator=g)
+    if xscale == "mixed":
+        X *= (10.0 ** (8 * torch.rand(shape[0], generator=g) - 4)).reshape(-1, *([1] * (len(shape) - 1)))
+        xscale = 1.0
+    else:
+        X *= xscale
     y = torch.randint(0, C, (shape[0],), generator=g)
     y[:C] = torch.arange(C)
     P = int(np.prod(shape[1:]))

@@ -47,6 +47,39 @@ def test_windowed_dataset_indexing(win_range):
         util.windowed_view(X, y[:-2], win_range)
 
 
+@pytest.mark.parametrize("win_range", [(-3, 4), (2, 6)])
+def test_windowed_dataloader_surface(win_range):
+    """The reference's loader surface (util.py:67-114): WindowedDataset is a torch Dataset whose
+    len() is the series length and which takes (and, like the reference, does not apply) transform
+    / target_transform; make_WindowedDataloader returns (dataloader, dataset, sampler) with a
+    SubsetRandomSampler over usable_idx, drop_last, and sample_shape = [batch_size] + window shape;
+    every batch stacks the reference's windows X[idx + w0 : idx + w1] and targets y[idx]."""
+    g = torch.Generator().manual_seed(1)
+    X = torch.randn(50, 4, 3, generator=g)
+    y = torch.randn(50, generator=g)
+    w0, w1 = win_range
+    ds = util.WindowedDataset(X, y, list(win_range), transform=lambda v: v * 0, target_transform=abs)
+    assert isinstance(ds, torch.utils.data.Dataset)
+    assert len(ds) == 50 and ds.n_windows == 50 - (w1 - w0) + 1
+    xi, yi = ds[int(ds.usable_idx[3])]
+    assert torch.equal(xi, X[int(ds.usable_idx[3]) + w0:int(ds.usable_idx[3]) + w1])  # not transformed
+    dl, ds2, sampler = util.make_WindowedDataloader(X, y, win_range=list(win_range), batch_size=8, drop_last=True)
+    assert isinstance(sampler, torch.utils.data.SubsetRandomSampler)
+    assert sorted(int(i) for i in sampler.indices) == ds2.usable_idx.tolist()
+    assert dl.sample_shape == [8, w1 - w0, 4, 3]
+    seen = []
+    usable = set(ds2.usable_idx.tolist())
+    for xb, yb in dl:
+        assert xb.shape == (8, w1 - w0, 4, 3) and yb.shape == (8,)
+        for k in range(8):
+            idx = int(torch.nonzero(y == yb[k])[0])  # (the targets are distinct draws)
+            if idx not in usable:  # a negative idx (w0 > 0): y[idx] wraps to the end, as in the reference
+                idx -= 50
+            assert idx in usable and torch.equal(xb[k], X[idx + w0: idx + w1])
+            seen.append(idx)
+    assert len(seen) == len(set(seen)) == (ds2.n_windows // 8) * 8  # each window once; drop_last
+
+
 @pytest.fixture()
 def _one_thread():
     n = torch.get_num_threads()

@@ -79,12 +79,21 @@ def main():
         if hasattr(_engine, name):
             timed(_engine, name, f"_engine.{name}")
     timed(_engine, "gradient_allreduce", "_engine.gradient_allreduce")
+    if hasattr(_engine, "RcclAllReduce"):
+        for name in ("max_f64", "broadcast", "barrier"):
+            if hasattr(_engine.RcclAllReduce, name):
+                timed(_engine.RcclAllReduce, name, f"RcclAllReduce.{name}")
     timed(_engine, "_adam_loop", "_engine._adam_loop")
 
-    def bracket(group):
+    comm = _engine.direct_comm(pg, 0) if hasattr(_engine, "direct_comm") else None
+
+    def bracket(group):  # as bench.py's timed region
         torch.cuda.synchronize()
         if group is not None:
-            dist.barrier()
+            if comm is not None:
+                comm.barrier()
+            else:
+                dist.barrier()
 
     fit(5, None)
     fit(5, pg)
