@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define TR_ABI_VERSION 6
+#define TR_ABI_VERSION 7
 
 #define TR_MODEL_LINEAR 0      /* CP_linear_regression: y_hat = <X, [[w; Phi]]> + bias, MSE */
 #define TR_MODEL_MULTINOMIAL 1 /* CP_logistic_regression: softmax(<X, [[w; Phi]]>), CE(weight) */
@@ -118,6 +118,25 @@ const char* tr_plan_describe(const tr_plan* plan);
  * paths, and a misaligned X on a vector plan is rejected with TR_E_ARG.
  */
 int tr_plan_set_x_stride(tr_plan* plan, int64_t stride);
+
+/*
+ * Range statistics of a sample-major X (n_rows rows of P floats at row stride xld; xld = 0: P):
+ * workgroup b of nblocks (1..1024) writes out[b] = max |x| and out[nblocks + b] = sum x^2 (double)
+ * over its rows, asynchronously on `stream`; the caller reduces the 2 * nblocks values.  One
+ * streaming read of X.  No reference counterpart: it guards a kernel's number format (below).
+ */
+int tr_x_range(const float* X, int64_t n_rows, int64_t P, int64_t xld, double* out, int nblocks, void* stream);
+
+/*
+ * X's range for the plan's next tr_loss_grad calls (max |x| and the mean of x^2 over X, e.g.
+ * from tr_x_range): the multinomial factored pass in its bf16-split form represents X as a bf16
+ * piece plus an f16 residual, within 2^-20 |x| + 2^-25 of x — normwise 2^-20 + 2^-25 / rms(X) —
+ * while rms(X) >= 2^-5 and max |x| < 2^23; outside that range (or for a non-finite value) the plan
+ * runs its exact form (three bf16 pieces, x represented exactly, ~15-20 % slower).  Re-set after
+ * every tr_plan_set_x_stride call (which resets the plan to the fast form).  Plans of other
+ * kernels ignore it.  The Python layer calls both once per X (Plan._x_form).
+ */
+int tr_plan_set_x_range(tr_plan* plan, double max_abs, double mean_sq);
 
 /*
  * Device status of the plan's kernels since the last call (synchronises the device).

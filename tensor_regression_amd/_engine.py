@@ -335,6 +335,42 @@ class Plan:
         if stride != getattr(self, "_xstride", 0):
             check(self.lib.tr_plan_set_x_stride(self.h, stride), "tr_plan_set_x_stride")
             self._xstride = stride
+            self._xrange_key = None  # (the re-chosen split body starts in its fast form)
+            self.describe = self.lib.tr_plan_describe(self.h).decode()
+
+    def _x_form(self, X):
+        """The multinomial split body's X form follows X's range (tr_plan_set_x_range): max |x| and
+        mean x^2 measured on the device (tr_x_range, one streaming read of X) once per X — keyed
+        by its data pointer, shape, strides and torch version counter, so a new or modified X is
+        measured again — and skipped for plans of other kernels.  X a util.HostStream: its host
+        copy's range, measured once (HostStream.range)."""
+        if "form=bf16split" not in self.describe:
+            return
+        from .util import HostStream
+        X = getattr(X, "_tr_stream", X)  # a HostStream chunk: the stream's host X
+        if isinstance(X, HostStream):
+            key = ("hoststream", id(X))
+            if key != getattr(self, "_xrange_key", None):
+                mx, msq = X.range()
+                check(self.lib.tr_plan_set_x_range(self.h, mx, msq), "tr_plan_set_x_range")
+                self._xrange_key = key
+                self.describe = self.lib.tr_plan_describe(self.h).decode()
+            return
+        key = (X.data_ptr(), tuple(X.shape), tuple(X.stride()), X._version)
+        if key == getattr(self, "_xrange_key", None):
+            return
+        N = int(X.shape[0])
+        P = int(np.prod(X.shape[1:]))
+        nb = int(min(1024, max(1, N)))
+        out = torch.empty(2 * nb, dtype=torch.float64, device=self.device_str)
+        ld = int(X.stride(0)) if N > 1 else P
+        check(self.lib.tr_x_range(ptr(X), N, P, ld, ptr(out), nb, stream_handle(self.dev)), "tr_x_range")
+        r = out.cpu().numpy()
+        mx = float(np.max(r[:nb])) if not np.isnan(r[:nb]).any() else float("nan")
+        msq = float(np.sum(r[nb:])) / max(1, N * P)
+        check(self.lib.tr_plan_set_x_range(self.h, mx, msq), "tr_plan_set_x_range")
+        self._xrange_key = key
+        self.describe = self.lib.tr_plan_describe(self.h).decode()
 
     def forward(self, X, arena, weights, out=None):
         N = X.shape[0]
@@ -350,6 +386,7 @@ class Plan:
 
     def loss_grad(self, X, target, class_weight, norm, arena, weights, grad, yhat=None, stop=None):
         self._set_stride(X)
+        self._x_form(X)
         if self.f64:
             rc = self.lib.tr_loss_grad_f64(self.h, ptr(X), X.shape[0], ptr(target), float(norm), ptr(arena),
                                            ptr(weights), ptr(grad), ptr(yhat), ptr(stop), stream_handle(self.dev))

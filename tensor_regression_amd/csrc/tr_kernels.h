@@ -75,6 +75,7 @@ hipError_t launch_linear_cluster(int CH, int S, int ncl, const float* X, int64_t
                                  unsigned long long* gran, uint32_t* err, const int32_t* stop, hipStream_t st);
 int rows_rb(int C);
 int cols_cw(int C);
+hipError_t launch_x_range(const float* X, int64_t N, int64_t P, int64_t xld, double* out, int nblocks, hipStream_t st);
 bool rows_supported(int C);
 hipError_t launch_rows(int C, int mode, int W, const float* X, int64_t N, int64_t P, int64_t xld,
                        const float* Bt, const float* bias, const void* target, const float* class_w,

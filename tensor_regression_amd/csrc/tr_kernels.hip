@@ -37,6 +37,51 @@ __device__ __forceinline__ float4 ldx(const float4* p) {
 __device__ __forceinline__ float ldx(const float* p) { return __builtin_nontemporal_load(p); }
 
 // ==========================================================================================
+// X range statistics (tr_x_range): max |x| and sum x^2 of the rows of workgroup b (rows b, b +
+// nblocks, ...), for the plan's choice of the multinomial split body's X form
+// ==========================================================================================
+__global__ __launch_bounds__(256) void k_x_range(const float* __restrict__ X, int64_t N, int64_t P, int64_t xld,
+                                                 double* __restrict__ out) {
+  __shared__ float smax[256];
+  __shared__ double ssum[256];
+  const int t = threadIdx.x;
+  float m = 0.f;
+  double s = 0.0;
+  for (int64_t n = blockIdx.x; n < N; n += gridDim.x) {
+    const float* row = X + n * xld;
+    float ps = 0.f;  // per-row partial in fp32 (<= P / 256 terms), accumulated in fp64
+    for (int64_t e = t; e < P; e += 256) {
+      const float v = ldx(row + e);
+      m = fmaxf(m, fabsf(v));
+      ps = fmaf(v, v, ps);
+      if (!(v == v)) m = v;  // a NaN is reported, not dropped by fmaxf
+    }
+    s += (double)ps;
+  }
+  smax[t] = m;
+  ssum[t] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (t < w) {
+      const float a = smax[t], b = smax[t + w];
+      smax[t] = (a != a || b != b) ? __builtin_nanf("") : fmaxf(a, b);
+      ssum[t] += ssum[t + w];
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    out[blockIdx.x] = (double)smax[0];
+    out[gridDim.x + blockIdx.x] = ssum[0];
+  }
+}
+
+hipError_t launch_x_range(const float* X, int64_t N, int64_t P, int64_t xld, double* out, int nblocks, hipStream_t st) {
+  if (nblocks < 1 || nblocks > 1024 || N < 0 || P < 1 || xld < P) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_x_range, dim3(nblocks), dim3(256), 0, st, X, N, P, xld, out);
+  return hipGetLastError();
+}
+
+// ==========================================================================================
 // K1a: factor preparation  (non_neg_fn, standard…py:53-85; multinomial…py:116-146)
 // ==========================================================================================
 __global__ __launch_bounds__(256) void k_prep_factors(FactorSet fs, const float* __restrict__ params,

@@ -46,6 +46,8 @@ struct MnlGeom {
   // 8 at rank <= 8 (other I, and J % 4 == 0 of 28..128, padded to the next), C <= 16; TR_DUO_SPLIT=1
   // takes it at (128, 64) / (64, 128) rank 5..8 too, =0 keeps the rank-block form): U partials at bs_oU
   int bsp, bs_oU;
+  // split body's X form (tr_plan_set_x_range): 0 = bf16 + f16 residual, 1 = three exact bf16 pieces
+  int bs_exact;
   // waves per workgroup and workgroups per CU of the two-workgroups-per-CU family (4, 2; the
   // split body on (32 NW, 64) and (16 NW, 128) samples: NW, 8 / NW)
   int du_nw, du_wpc;

@@ -158,8 +158,9 @@ typedef _Float16 bs_h2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t bs_pack_h(float a, float b) {
   return __builtin_bit_cast(uint32_t, bs_h2{(_Float16)a, (_Float16)b});
 }
-__device__ __forceinline__ du_f32x4 bs_mfma_h(sl_u4 a, sl_u4 bb, du_f32x4 c) {
-  if (TR_DUO_SKIP & 2) return c + __uint_as_float(a[0]) * __uint_as_float(bb[0]);
+__device__ __forceinline__ du_f32x4 bs_mfma_h(sl_u4 a, const uint32_t (&b)[4], du_f32x4 c) {
+  if (TR_DUO_SKIP & 2) return c + __uint_as_float(a[0]) * __uint_as_float(b[0]);
+  const sl_u4 bb = sl_u4{b[0], b[1], b[2], b[3]};
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(bs_h8, a), __builtin_bit_cast(bs_h8, bb), c, 0, 0,
                                                 0);
 }
@@ -529,22 +530,21 @@ __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, cons
 // MFMAs with the fp32 operands split into round-to-nearest pieces, as the spectral slice kernel
 // does (tr_spectral_slice.hip "bf16 split"); the factors in three bf16 pieces and the rank columns
 // packed, B12 = [b1 | b2] (columns 0-7 | 8-15, rank = column & 7), B3 = [b3 | 0], so that one
-// 16-wide MFMA carries two piece products (columns r and r + 8 are folded at the end).  X, per
-// wave and sample, in one of two forms chosen from the wave's own operands (all in registers
-// before its GEMM steps):
-//  - fast (every sample whose largest |x| in the wave lies in [2^-5, 2^24)): x1 = bf16(x) and ONE
-//    f16 piece x2 = f16(x - x1) against H = [f16(phi) | f16(phi - f16(phi))]: x1 + x2 is within
-//    2^-20 of the wave's largest |x| (an f16 residual of an element much smaller than that loses
-//    bits, but only below 2^-25 absolute), three MFMAs per tile and k step:
+// 16-wide MFMA carries two piece products (columns r and r + 8 are folded at the end).  X in one
+// of two forms, a template parameter the plan sets from X's range (tr_plan_set_x_range):
+//  - fast (EXACT = false): x1 = bf16(x) and ONE f16 piece x2 = f16(x - x1), against
+//    H = [f16(phi) | f16(phi - f16(phi))]; three MFMAs per tile and k step:
 //      acc += x2.H + x1.B3 + x1.B12   (= x1b1 + x1b2 + x1b3 + x2 phi)
-//  - exact (any other sample, e.g. data in small units or large raw counts, where the f16 residual
-//    would lose precision or overflow to inf): x = x1 + x2 + x3 EXACTLY in bf16 pieces (x2 =
-//    bf16(x - x1), x3 = x - x1 - x2: at most 8 significant bits; bf16 has fp32's exponent range),
-//    four MFMAs:  acc += x3.B12 + x2.B12 + x1.B3 + x1.B12 (dropped: x2b3, x3b3, < 2^-24 |xb|).
-// The exact form alone costs 15-20 % on these shapes (issue-bound: 11 instead of 6 VALU per pair
-// of X values); the range test, a max over the wave's operand registers and two ballots, costs
-// ~1 % (round 6, gpurun_out/r06b).  tests/test_gpu_parity.py::test_multinomial_split_body_x_scale
-// runs both forms at X scales 1e-4 .. 3e7.
+//    x1 + x2 is within 2^-20 |x| + 2^-25 of x (the f16 residual of |x| < 2^-5 is subnormal, of
+//    |x| >= 2^24 it overflows): normwise over X within 2^-20 + 2^-25 / rms(X), so the plan takes
+//    it only while rms(X) >= 2^-5 and max |X| < 2^23;
+//  - exact (EXACT = true, any other X: data in small units, large raw counts): x = x1 + x2 + x3
+//    EXACTLY in bf16 pieces (x2 = bf16(x - x1), x3 = x - x1 - x2, at most 8 significant bits;
+//    bf16 has fp32's exponent range), four MFMAs:
+//      acc += x3.B12 + x2.B12 + x1.B3 + x1.B12   (dropped: x2b3, x3b3, < 2^-24 |xb|)
+//    15-20 % slower on these shapes (11 instead of 6 VALU per pair of X values: issue-bound).
+// Round 5 ran the fast form on any X: 2e-4 off at |X| ~ 1e-4, inf above 2^24
+// (tests/test_gpu_parity.py::test_multinomial_split_body_x_scale runs both forms at 1e-4 .. 3e7).
 // A 32 KiB sample takes 96 MFMAs per workgroup instead of 512 4x4x1 ones: the rank-block form
 // spends 1,024 issue cycles per wave-sample on MFMAs alone.  J = 64 samples of 32 NW rows run NW
 // waves (NW = 2..8), J = 128 ones of 16 NW rows NW waves (NW = 4, 6, 8); 8 / NW workgroups per
@@ -559,7 +559,7 @@ __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, cons
 // wave's i k-step, and dPhi1 = sum_n Wv_n V_n is linear in it: the waves' partials are summed
 // once, at the end.  Every wave runs the softmax epilogue of the previous sample (staged between
 // its GEMM steps) for all 8 ranks; wave 0 alone accumulates dPhiC and the loss.
-template <int JT, int NW, int NS, bool PAD>
+template <int JT, int NW, int NS, bool PAD, bool EXACT>
 __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, const int64_t* __restrict__ lab,
                                          const float* __restrict__ class_w, float* lds, const int wv, const int lane) {
   const int t = threadIdx.x;
@@ -587,35 +587,39 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
   const bool cok = c < C;
   const float cwl = cok ? class_w[c] : 0.f;
   const float NEG = -__builtin_huge_valf();
+  float gsel[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) gsel[q] = gq == q ? 1.f : 0.f;
+  float rsel[8];  // 1 where this lane's accumulator rank (n & 7) == r
+#pragma unroll
+  for (int r = 0; r < 8; ++r) rsel[r] = r8 == r ? 1.f : 0.f;
 
   const int it0 = NT == 2 ? 32 * wv : 16 * wv;                    // first T row of this wave
   const int iv0 = JT == 64 ? 32 * wv : 32 * (wv % NKS);           // V k-step (rows) of this wave
   const int cv = n + (J == 128 ? 16 * (wv / NKS) : 0);            // V chunk (j = 4 cv + tile)
   // B operands, split once per launch: T (Phi1, element e of lane group gq <-> j = 32 s + 8 gq + e)
-  // (the fast form's f16 pieces of Phi1, hT, are the same for every wave: one table in the rank-block
-  // body's Phi1^T area, which this body does not use, read per T step; hV stays in registers)
-  uint32_t* sH = reinterpret_cast<uint32_t*>(lds + g.du_oP1);  // [NKT][64 lanes][4]
-  uint32_t bT12[NKT][4], bT3[NKT][4], bV12[4], bV3[4], hV[4];
+  uint32_t bT12[NKT][4], bT3[NKT][4], hT[NKT][4], bV12[4], bV3[4], hV[4];
   auto bsplit = [&](float x0, float x1, uint32_t& b12, uint32_t& b3, uint32_t& hh) {
     uint32_t h1, h2, h3;
     sl_split2(x0, x1, h1, h2, h3);
     b12 = lo8 ? h1 : h2;
     b3 = lo8 ? h3 : 0u;
-    // f16 pieces for the fast form's f16 X piece: [f16(x) | f16(x - f16(x))]
-    const uint32_t f1 = bs_pack_h(x0, x1);
-    const bs_h2 f1v = __builtin_bit_cast(bs_h2, f1);
-    const uint32_t f2 = bs_pack_h(x0 - (float)f1v[0], x1 - (float)f1v[1]);
-    hh = lo8 ? f1 : f2;
+    if constexpr (!EXACT) {  // f16 pieces for the fast form's f16 X piece: [f16(x) | f16(x - f16(x))]
+      const uint32_t f1 = bs_pack_h(x0, x1);
+      const bs_h2 f1v = __builtin_bit_cast(bs_h2, f1);
+      const uint32_t f2 = bs_pack_h(x0 - (float)f1v[0], x1 - (float)f1v[1]);
+      hh = lo8 ? f1 : f2;
+    } else {
+      hh = 0u;
+    }
   };
 #pragma unroll
   for (int s = 0; s < NKT; ++s)
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
       const int j = 32 * s + 8 * gq + 2 * v;
-      uint32_t hh;
       bsplit((rok && (!PAD || j < Jr)) ? P1[(int64_t)j * R + r8] : 0.f,
-             (rok && (!PAD || j + 1 < Jr)) ? P1[(int64_t)(j + 1) * R + r8] : 0.f, bT12[s][v], bT3[s][v], hh);
-      if (wv == 0) sH[(s * TR_WAVE + lane) * 4 + v] = hh;
+             (rok && (!PAD || j + 1 < Jr)) ? P1[(int64_t)(j + 1) * R + r8] : 0.f, bT12[s][v], bT3[s][v], hT[s][v]);
     }
 #pragma unroll
   for (int v = 0; v < 4; ++v) {  // V (Phi0, element e <-> i = iv0 + 8 gq + e)
@@ -748,9 +752,9 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
       // Wv[r] of this lane's accumulator rank r = n & 7 (rank r < 4: row r's e_w0, else row r - 4's e_w1)
       float wv8 = 0.f;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {  // (lane selects, not 0/1 weights held in 12 registers)
-        wv8 = r8 == r ? du_rdl(e_w0, 16 * r) : wv8;
-        wv8 = r8 == r + 4 ? du_rdl(e_w1, 16 * r) : wv8;
+      for (int r = 0; r < 4; ++r) {
+        wv8 = fmaf(du_rdl(e_w0, 16 * r), rsel[r], wv8);
+        wv8 = fmaf(du_rdl(e_w1, 16 * r), rsel[r + 4], wv8);
       }
       e_wv = wv8;
     } else {
@@ -759,8 +763,8 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
 #pragma unroll
       for (int q = 0; q < 4; ++q) gV[q] += e_wv * VP[q];
       if (wv == 0) {  // dPhiC[c][r] += dZ[c] w_r U[r], r = gq, gq + 4
-        const float u0 = gq == 0 ? uR[0] : gq == 1 ? uR[1] : gq == 2 ? uR[2] : uR[3];
-        const float u1 = gq == 0 ? uR[4] : gq == 1 ? uR[5] : gq == 2 ? uR[6] : uR[7];
+        const float u0 = fmaf(uR[3], gsel[3], fmaf(uR[2], gsel[2], fmaf(uR[1], gsel[1], uR[0] * gsel[0])));
+        const float u1 = fmaf(uR[7], gsel[3], fmaf(uR[6], gsel[2], fmaf(uR[5], gsel[1], uR[4] * gsel[0])));
         dpc0 = fmaf(e_dz, wg0 * u0, dpc0);
         dpc1 = fmaf(e_dz, wg1 * u1, dpc1);
       }
@@ -820,61 +824,48 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
       xt[u][0] = *reinterpret_cast<const du_f32x4*>(sb + tro[tt] + 4 * (q0 ^ tsw));
       xt[u][1] = *reinterpret_cast<const du_f32x4*>(sb + tro[tt] + 4 * ((q0 + 1) ^ tsw));
     }
-    // the form of this wave's X pieces for sample k (wave-uniform, from its operands, all in
-    // registers now): fast unless its largest |x| lies outside [2^-5, 2^24) or is not finite
-    float xm = 0.f;
-#pragma unroll
-    for (int e = 0; e < 8; ++e)
-      xm = fmaxf(fmaxf(xm, fmaxf(fabsf(xv[e][0]), fabsf(xv[e][1]))), fmaxf(fabsf(xv[e][2]), fabsf(xv[e][3])));
-#pragma unroll
-    for (int u = 0; u < NU; ++u)
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-        xm = fmaxf(fmaxf(xm, fmaxf(fabsf(xt[u][h][0]), fabsf(xt[u][h][1]))),
-                   fmaxf(fabsf(xt[u][h][2]), fabsf(xt[u][h][3])));
-    const bool fast = __builtin_amdgcn_ballot_w64(!(xm < 0x1p24f)) == 0 && __builtin_amdgcn_ballot_w64(xm >= 0x1p-5f) != 0;
 #pragma unroll
     for (int st = 0; st < NU + 4; ++st) {
       if (!(TR_DUO_SKIP & 8)) dma_piece(goff[st], psrc, pm0 + (uint32_t)st * (uint32_t)(NW * 1024));
-      // the k step's eight X values of this lane (T: a row's two quads; V: element tv of eight rows)
-      float ev[8];
-      if (st < NU) {
-#pragma unroll
-        for (int v = 0; v < 8; ++v) ev[v] = xt[st][v >> 2][v & 3];
-      } else {
-#pragma unroll
-        for (int v = 0; v < 8; ++v) ev[v] = xv[v][st - NU];
-      }
-      const int tt = st / NKT, s = st - tt * NKT;
-      du_f32x4& acc = st < NU ? aT[tt] : aV[st - NU];
-      const uint32_t(&b12)[4] = st < NU ? bT12[s] : bV12;
-      const uint32_t(&b3)[4] = st < NU ? bT3[s] : bV3;
-      sl_u4 x1, x2;
-      if (fast) {  // x1 = bf16(x), x2 = f16(x - x1): acc += x2.H + x1.B3 + x1.B12 (smallest first)
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          const uint32_t h = sl_pack_rne(ev[2 * v], ev[2 * v + 1]);
-          x1[v] = h;
-          x2[v] = bs_pack_h(ev[2 * v] - sl_lo_f32(h), ev[2 * v + 1] - sl_hi_f32(h));
-        }
-        const sl_u4 hh = st < NU ? *reinterpret_cast<const sl_u4*>(sH + (s * TR_WAVE + lane) * 4)
-                                 : sl_u4{hV[0], hV[1], hV[2], hV[3]};
-        acc = bs_mfma_h(x2, hh, acc);
-      } else {  // exact: x = x1 + x2 + x3 in bf16: acc += x3.B12 + x2.B12 + x1.B3 + x1.B12
-        sl_u4 x3;
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
+      sl_u4 x1, x2, x3;  // the k step's X pieces (pairs per VGPR)
+      auto split = [&](float e0, float e1, int v) {
+        if constexpr (EXACT) {
           uint32_t h1, h2, h3;
-          sl_split2(ev[2 * v], ev[2 * v + 1], h1, h2, h3);
+          sl_split2(e0, e1, h1, h2, h3);
           x1[v] = h1;
           x2[v] = h2;
           x3[v] = h3;
+        } else {
+          const uint32_t h = sl_pack_rne(e0, e1);
+          x1[v] = h;
+          x2[v] = bs_pack_h(e0 - sl_lo_f32(h), e1 - sl_hi_f32(h));
         }
-        acc = bs_mfma(x3, b12, acc);
-        acc = bs_mfma(x2, b12, acc);
+      };
+      // smallest products first into the accumulator
+      auto gemm = [&](du_f32x4& acc, const uint32_t (&b12)[4], const uint32_t (&b3)[4], const uint32_t (&hh)[4]) {
+        if constexpr (EXACT) {
+          acc = bs_mfma(x3, b12, acc);
+          acc = bs_mfma(x2, b12, acc);
+        } else {
+          acc = bs_mfma_h(x2, hh, acc);
+        }
+        acc = bs_mfma(x1, b3, acc);
+        acc = bs_mfma(x1, b12, acc);
+      };
+      if (st < NU) {
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const du_f32x4& xr = xt[st][v >> 1];
+          split(xr[2 * (v & 1)], xr[2 * (v & 1) + 1], v);
+        }
+        const int tt = st / NKT, s = st - tt * NKT;
+        gemm(aT[tt], bT12[s], bT3[s], hT[s]);
+      } else {
+        const int tv = st - NU;  // j-tile: element tv of each row's chunk
+#pragma unroll
+        for (int v = 0; v < 4; ++v) split(xv[2 * v][tv], xv[2 * v + 1][tv], v);
+        gemm(aV[tv], bV12, bV3, hV);
       }
-      acc = bs_mfma(x1, b3, acc);
-      acc = bs_mfma(x1, b12, acc);
       if (st >= 1 && st <= 7) epi(st, PS, yP, cwP);
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -957,7 +948,7 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
 
 // NW waves per workgroup, 8 / NW workgroups per CU (the second bound is waves per SIMD: two,
 // 256 VGPRs each), a ring of NS samples
-template <int JT, int NW, int NS, bool PAD>
+template <int JT, int NW, int NS, bool PAD, bool EXACT>
 __global__ __launch_bounds__(NW * TR_WAVE, 2) void k_mnl_bsp(MnlGeom g, DuArgs a, const int64_t* __restrict__ lab,
                                                                const float* __restrict__ class_w,
                                                                const int32_t* __restrict__ stop) {
@@ -965,7 +956,7 @@ __global__ __launch_bounds__(NW * TR_WAVE, 2) void k_mnl_bsp(MnlGeom g, DuArgs a
   if (stop != nullptr && *stop != 0) return;
   const int lane = threadIdx.x & (TR_WAVE - 1);
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / TR_WAVE);
-  bsp_body<JT, NW, NS, PAD>(g, a, lab, class_w, lds, wv, lane);
+  bsp_body<JT, NW, NS, PAD, EXACT>(g, a, lab, class_w, lds, wv, lane);
 }
 
 template <int JT>
@@ -986,12 +977,16 @@ __global__ __launch_bounds__(DU_T, 2) void k_mnl_duo(MnlGeom g, DuArgs a, const 
 #define TR_BSP_LIST(X) \
   X(64, 2, 2) X(64, 3, 2) X(64, 4, 2) X(64, 5, 2) X(64, 5, 3) X(64, 6, 2) X(64, 6, 3) X(64, 7, 2) \
   X(64, 8, 2) X(128, 4, 2) X(128, 6, 2) X(128, 6, 3) X(128, 8, 2)
-static const void* duo_kernel(const MnlGeom& g) {
+static const void* duo_kernel(const MnlGeom& g, bool exact) {
   if (g.bsp) {
 #define TR_BSP_PTR(J_, NW_, NS_)                                                                          \
-  if (g.du_jt == J_ && g.du_nw == NW_ && g.du_ns == NS_)                                                   \
-    return g.du_pad ? reinterpret_cast<const void*>(&k_mnl_bsp<J_, NW_, NS_, true>)                        \
-                    : reinterpret_cast<const void*>(&k_mnl_bsp<J_, NW_, NS_, false>);
+  if (g.du_jt == J_ && g.du_nw == NW_ && g.du_ns == NS_) {                                                 \
+    if (exact)                                                                                            \
+      return g.du_pad ? reinterpret_cast<const void*>(&k_mnl_bsp<J_, NW_, NS_, true, true>)                \
+                      : reinterpret_cast<const void*>(&k_mnl_bsp<J_, NW_, NS_, false, true>);              \
+    return g.du_pad ? reinterpret_cast<const void*>(&k_mnl_bsp<J_, NW_, NS_, true, false>)                 \
+                    : reinterpret_cast<const void*>(&k_mnl_bsp<J_, NW_, NS_, false, false>);               \
+  }
     TR_BSP_LIST(TR_BSP_PTR)
 #undef TR_BSP_PTR
     return nullptr;
@@ -1018,6 +1013,7 @@ static int64_t duo_carve(MnlGeom* g, int nw, int64_t spf, int ns) {
 void mnl_duo_geom(MnlGeom* g) {
   g->duo = 0;
   g->bsp = 0;
+  g->bs_exact = 0;
   g->du_nw = 4;
   g->du_wpc = 2;
   g->du_ns = 2;
@@ -1080,22 +1076,27 @@ void mnl_duo_geom(MnlGeom* g) {
   g->bsp = bsp ? 1 : 0;
 }
 
+// the body g describes runs without spills at du_wpc workgroups per CU (the split body in both of
+// its X forms: the plan picks one per X, tr_plan_set_x_range)
 static hipError_t duo_kernel_ok(const MnlGeom& g, bool* ok) {
-  const void* k = duo_kernel(g);
-  if (k == nullptr) {
-    *ok = false;
-    return hipSuccess;
+  *ok = true;
+  for (int form = 0; form < (g.bsp ? 2 : 1) && *ok; ++form) {
+    const void* k = duo_kernel(g, form == 1);
+    if (k == nullptr) {
+      *ok = false;
+      return hipSuccess;
+    }
+    const size_t lds = (size_t)g.du_lds_floats * 4;
+    hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    hipFuncAttributes attr;
+    e = hipFuncGetAttributes(&attr, k);
+    if (e != hipSuccess) return e;
+    int nb = 0;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, g.du_nw * TR_WAVE, lds);
+    if (e != hipSuccess) return e;
+    *ok = attr.localSizeBytes == 0 && nb >= g.du_wpc;  // no spills, du_wpc per CU
   }
-  const size_t lds = (size_t)g.du_lds_floats * 4;
-  hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  if (e != hipSuccess) return e;
-  hipFuncAttributes attr;
-  e = hipFuncGetAttributes(&attr, k);
-  if (e != hipSuccess) return e;
-  int nb = 0;
-  e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, g.du_nw * TR_WAVE, lds);
-  if (e != hipSuccess) return e;
-  *ok = attr.localSizeBytes == 0 && nb >= g.du_wpc;  // no spills, du_wpc per CU
   return hipSuccess;
 }
 
@@ -1144,12 +1145,18 @@ hipError_t launch_mnl_duo(const MnlGeom& g, int grid, const float* X, int64_t N,
   if (g.bsp) {
 #define TR_BSP_LAUNCH(J_, NW_, NS_)                                                                       \
   if (g.du_jt == J_ && g.du_nw == NW_ && g.du_ns == NS_) {                                                 \
-    if (g.du_pad)                                                                                         \
-      hipLaunchKernelGGL((k_mnl_bsp<J_, NW_, NS_, true>), dim3(grid), dim3(NW_ * TR_WAVE), lds, st, g, a, lab, \
-                         class_w, stop);                                                                  \
+    if (g.du_pad && g.bs_exact)                                                                           \
+      hipLaunchKernelGGL((k_mnl_bsp<J_, NW_, NS_, true, true>), dim3(grid), dim3(NW_ * TR_WAVE), lds, st, g, a, \
+                         lab, class_w, stop);                                                             \
+    else if (g.du_pad)                                                                                    \
+      hipLaunchKernelGGL((k_mnl_bsp<J_, NW_, NS_, true, false>), dim3(grid), dim3(NW_ * TR_WAVE), lds, st, g, a, \
+                         lab, class_w, stop);                                                             \
+    else if (g.bs_exact)                                                                                  \
+      hipLaunchKernelGGL((k_mnl_bsp<J_, NW_, NS_, false, true>), dim3(grid), dim3(NW_ * TR_WAVE), lds, st, g, a, \
+                         lab, class_w, stop);                                                             \
     else                                                                                                  \
-      hipLaunchKernelGGL((k_mnl_bsp<J_, NW_, NS_, false>), dim3(grid), dim3(NW_ * TR_WAVE), lds, st, g, a, lab, \
-                         class_w, stop);                                                                  \
+      hipLaunchKernelGGL((k_mnl_bsp<J_, NW_, NS_, false, false>), dim3(grid), dim3(NW_ * TR_WAVE), lds, st, g, \
+                         a, lab, class_w, stop);                                                          \
     return hipGetLastError();                                                                             \
   }
     TR_BSP_LIST(TR_BSP_LAUNCH)

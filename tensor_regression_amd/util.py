@@ -139,6 +139,17 @@ class HostStream:
     def __len__(self):
         return self.shape[0]
 
+    def range(self):
+        """(max |x|, mean x^2) of the host X, computed once (the plan's X-form choice for the
+        multinomial split body, Plan._x_form; the chunks are not measured one by one)."""
+        if getattr(self, "_range", None) is None:
+            a = self.X.reshape(-1)
+            mx = float(a.abs().max()) if a.numel() else 0.0
+            if bool(torch.isnan(a).any()):
+                mx = float("nan")
+            self._range = (mx, float(a.double().square().mean()) if a.numel() else 0.0)
+        return self._range
+
     @property
     def ndim(self):
         return len(self.shape)
@@ -171,8 +182,10 @@ class HostStream:
                 issue(c + 1)
             b = c % 2
             compute.wait_event(self.copied[b])
+            Xc = self.bufs[b][: r1 - r0]
+            Xc._tr_stream = self  # (Plan._x_form takes the whole host X's range, not the chunk's)
             try:
-                yield r0, r1, self.bufs[b][: r1 - r0]
+                yield r0, r1, Xc
             finally:
                 # also when the consumer raises or abandons the pass: the kernels it already
                 # queued on this buffer must finish before a later pass copies into it

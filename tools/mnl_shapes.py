@@ -14,7 +14,8 @@ import sys
 import numpy as np
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# TR_PKG_ROOT: another copy of the package (an earlier round's, with TR_HIP_LIB its library) for A/B
+sys.path.insert(0, os.environ.get("TR_PKG_ROOT", os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from tensor_regression_amd import CP_logistic_regression  # noqa: E402
 
 dev = "cuda:0"
