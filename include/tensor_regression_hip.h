@@ -120,23 +120,30 @@ const char* tr_plan_describe(const tr_plan* plan);
 int tr_plan_set_x_stride(tr_plan* plan, int64_t stride);
 
 /*
- * Range statistics of a sample-major X (n_rows rows of P floats at row stride xld; xld = 0: P):
- * workgroup b of nblocks (1..1024) writes out[b] = max |x| and out[nblocks + b] = sum x^2 (double)
- * over its rows, asynchronously on `stream`; the caller reduces the 2 * nblocks values.  One
- * streaming read of X.  No reference counterpart: it guards a kernel's number format (below).
+ * Range statistics of a sample-major X (n_rows rows of P floats at row stride xld; xld = 0: P;
+ * rows may overlap): workgroup b of nblocks (1..1024) writes out[b] = max |x|,
+ * out[nblocks + b] = the smallest mean x^2 of a row that is not all zero (+inf if none) and
+ * out[2 nblocks + b] = min x (doubles) over its rows, asynchronously on `stream`; the caller
+ * reduces the 3 * nblocks values (max, min, min).  One streaming read of X.  No reference
+ * counterpart: it guards the split kernels' number formats (tr_plan_set_x_range).
  */
 int tr_x_range(const float* X, int64_t n_rows, int64_t P, int64_t xld, double* out, int nblocks, void* stream);
 
 /*
- * X's range for the plan's next tr_loss_grad calls (max |x| and the mean of x^2 over X, e.g.
- * from tr_x_range): the multinomial factored pass in its bf16-split form represents X as a bf16
- * piece plus an f16 residual, within 2^-20 |x| + 2^-25 of x — normwise 2^-20 + 2^-25 / rms(X) —
- * while rms(X) >= 2^-5 and max |x| < 2^23; outside that range (or for a non-finite value) the plan
- * runs its exact form (three bf16 pieces, x represented exactly, ~15-20 % slower).  Re-set after
- * every tr_plan_set_x_stride call (which resets the plan to the fast form).  Plans of other
- * kernels ignore it.  The Python layer calls both once per X (Plan._x_form).
+ * X's range for the plan's next tr_loss_grad calls (max |x|, the smallest mean x^2 of a nonzero
+ * sample, and min x, e.g. from tr_x_range).
+ *  - The multinomial factored pass in its bf16-split form represents X as a bf16 piece plus an f16
+ *    residual, within 2^-20 |x| + 2^-25 of x — per sample normwise 2^-20 + 2^-25 / rms(sample) —
+ *    while every nonzero sample's rms >= 2^-5 and max |x| < 2^23; outside that range (or for a
+ *    non-finite value) the plan runs its exact form (three bf16 pieces, x represented exactly,
+ *    ~15-20 % slower).
+ *  - The spectral column-slice kernel in its split form takes X in two bf16 pieces; on signed X
+ *    (min x < 0: the forward T = X Phi0 cancels) the plan runs its signed form (the forward's X in
+ *    three pieces and per-sample gradient accumulators, ~13 % slower).
+ * Re-set after every tr_plan_set_x_stride call (which resets the plan to its default form).
+ * Plans of other kernels ignore it.  The Python layer calls both once per X (Plan._x_form).
  */
-int tr_plan_set_x_range(tr_plan* plan, double max_abs, double mean_sq);
+int tr_plan_set_x_range(tr_plan* plan, double max_abs, double min_row_mean_sq, double min_x);
 
 /*
  * Device status of the plan's kernels since the last call (synchronises the device).

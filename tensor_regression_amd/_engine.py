@@ -339,20 +339,21 @@ class Plan:
             self.describe = self.lib.tr_plan_describe(self.h).decode()
 
     def _x_form(self, X):
-        """The multinomial split body's X form follows X's range (tr_plan_set_x_range): max |x| and
-        mean x^2 measured on the device (tr_x_range, one streaming read of X) once per X — keyed
+        """The split kernels' X form follows X's range (tr_plan_set_x_range): max |x|, min x and the
+        smallest mean x^2 of a nonzero sample, measured on the device (tr_x_range, one streaming
+        read of X) once per X — keyed
         by its data pointer, shape, strides and torch version counter, so a new or modified X is
         measured again — and skipped for plans of other kernels.  X a util.HostStream: its host
         copy's range, measured once (HostStream.range)."""
-        if "form=bf16split" not in self.describe:
+        if "form=bf16split" not in self.describe and "bf16split" not in self.describe:
             return
         from .util import HostStream
         X = getattr(X, "_tr_stream", X)  # a HostStream chunk: the stream's host X
         if isinstance(X, HostStream):
             key = ("hoststream", id(X))
             if key != getattr(self, "_xrange_key", None):
-                mx, msq = X.range()
-                check(self.lib.tr_plan_set_x_range(self.h, mx, msq), "tr_plan_set_x_range")
+                mx, msq, mn = X.range()
+                check(self.lib.tr_plan_set_x_range(self.h, mx, msq, mn), "tr_plan_set_x_range")
                 self._xrange_key = key
                 self.describe = self.lib.tr_plan_describe(self.h).decode()
             return
@@ -362,13 +363,14 @@ class Plan:
         N = int(X.shape[0])
         P = int(np.prod(X.shape[1:]))
         nb = int(min(1024, max(1, N)))
-        out = torch.empty(2 * nb, dtype=torch.float64, device=self.device_str)
+        out = torch.empty(3 * nb, dtype=torch.float64, device=self.device_str)
         ld = int(X.stride(0)) if N > 1 else P
         check(self.lib.tr_x_range(ptr(X), N, P, ld, ptr(out), nb, stream_handle(self.dev)), "tr_x_range")
         r = out.cpu().numpy()
         mx = float(np.max(r[:nb])) if not np.isnan(r[:nb]).any() else float("nan")
-        msq = float(np.sum(r[nb:])) / max(1, N * P)
-        check(self.lib.tr_plan_set_x_range(self.h, mx, msq), "tr_plan_set_x_range")
+        msq = float(np.min(r[nb:2 * nb]))  # the smallest mean x^2 of a nonzero sample
+        mn = float(np.min(r[2 * nb:]))
+        check(self.lib.tr_plan_set_x_range(self.h, mx, msq, mn), "tr_plan_set_x_range")
         self._xrange_key = key
         self.describe = self.lib.tr_plan_describe(self.h).decode()
 

@@ -50,7 +50,7 @@ SIGNATURES = {
     "tr_spectral_latents": (_c.c_int, [_vp, _vp, _c.c_int64, _vp, _vp, _vp]),
     "tr_plan_set_x_stride": (_c.c_int, [_vp, _c.c_int64]),
     "tr_x_range": (_c.c_int, [_vp, _c.c_int64, _c.c_int64, _c.c_int64, _vp, _c.c_int, _vp]),
-    "tr_plan_set_x_range": (_c.c_int, [_vp, _c.c_double, _c.c_double]),
+    "tr_plan_set_x_range": (_c.c_int, [_vp, _c.c_double, _c.c_double, _c.c_double]),
     "tr_plan_status": (_c.c_int, [_vp, _c.POINTER(_c.c_int32)]),
     "tr_adam_step": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _c.c_float, _c.c_double, _c.c_double,
                                 _c.c_double, _c.c_double, _c.c_double, _c.c_int, _c.c_int64, _vp,

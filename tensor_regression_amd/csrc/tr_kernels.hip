@@ -37,46 +37,56 @@ __device__ __forceinline__ float4 ldx(const float4* p) {
 __device__ __forceinline__ float ldx(const float* p) { return __builtin_nontemporal_load(p); }
 
 // ==========================================================================================
-// X range statistics (tr_x_range): max |x| and sum x^2 of the rows of workgroup b (rows b, b +
-// nblocks, ...), for the plan's choice of the multinomial split body's X form
+// X range statistics (tr_x_range), for the plan's choice of its split kernels' X form: over the
+// rows of workgroup b (one wave per row: rows 4 b + w, 4 b + w + 4 nblocks, ...) max |x|, min x,
+// and the smallest mean x^2 of a row that is not all zero
 // ==========================================================================================
 __global__ __launch_bounds__(256) void k_x_range(const float* __restrict__ X, int64_t N, int64_t P, int64_t xld,
                                                  double* __restrict__ out) {
-  __shared__ float smax[256];
-  __shared__ double ssum[256];
-  const int t = threadIdx.x;
-  float m = 0.f;
-  double s = 0.0;
-  for (int64_t n = blockIdx.x; n < N; n += gridDim.x) {
+  __shared__ float smax[4], smin[4];
+  __shared__ double sms[4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float m = 0.f, mn = __builtin_huge_valf();
+  double rms_min = __builtin_huge_val();
+  for (int64_t n = 4 * (int64_t)blockIdx.x + w; n < N; n += 4 * (int64_t)gridDim.x) {
     const float* row = X + n * xld;
-    float ps = 0.f;  // per-row partial in fp32 (<= P / 256 terms), accumulated in fp64
-    for (int64_t e = t; e < P; e += 256) {
+    double ps = 0.0;
+    for (int64_t e = lane; e < P; e += 64) {
       const float v = ldx(row + e);
-      m = fmaxf(m, fabsf(v));
-      ps = fmaf(v, v, ps);
-      if (!(v == v)) m = v;  // a NaN is reported, not dropped by fmaxf
+      m = (v != v) ? v : fmaxf(m, fabsf(v));  // a NaN is reported, not dropped by fmaxf
+      mn = fminf(mn, v);
+      ps += (double)v * (double)v;
     }
-    s += (double)ps;
+    for (int o = 32; o > 0; o >>= 1) ps += __shfl_xor(ps, o, 64);
+    if (ps > 0.0) rms_min = fmin(rms_min, ps / (double)P);
   }
-  smax[t] = m;
-  ssum[t] = s;
+  for (int o = 32; o > 0; o >>= 1) {
+    const float a = __shfl_xor(m, o, 64);
+    m = (m != m || a != a) ? __builtin_nanf("") : fmaxf(m, a);
+    mn = fminf(mn, __shfl_xor(mn, o, 64));
+  }
+  if (lane == 0) {
+    smax[w] = m;
+    smin[w] = mn;
+    sms[w] = rms_min;
+  }
   __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
-    if (t < w) {
-      const float a = smax[t], b = smax[t + w];
-      smax[t] = (a != a || b != b) ? __builtin_nanf("") : fmaxf(a, b);
-      ssum[t] += ssum[t + w];
+  if (threadIdx.x == 0) {
+    float a = smax[0], b = smin[0];
+    double c = sms[0];
+    for (int k = 1; k < 4; ++k) {
+      a = (a != a || smax[k] != smax[k]) ? __builtin_nanf("") : fmaxf(a, smax[k]);
+      b = fminf(b, smin[k]);
+      c = fmin(c, sms[k]);
     }
-    __syncthreads();
-  }
-  if (t == 0) {
-    out[blockIdx.x] = (double)smax[0];
-    out[gridDim.x + blockIdx.x] = ssum[0];
+    out[blockIdx.x] = (double)a;
+    out[gridDim.x + blockIdx.x] = c;
+    out[2 * gridDim.x + blockIdx.x] = (double)b;
   }
 }
 
 hipError_t launch_x_range(const float* X, int64_t N, int64_t P, int64_t xld, double* out, int nblocks, hipStream_t st) {
-  if (nblocks < 1 || nblocks > 1024 || N < 0 || P < 1 || xld < P) return hipErrorInvalidValue;
+  if (nblocks < 1 || nblocks > 1024 || N < 0 || P < 1 || xld < 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_x_range, dim3(nblocks), dim3(256), 0, st, X, N, P, xld, out);
   return hipGetLastError();
 }

@@ -42,7 +42,9 @@ struct SpecGeom {
   int gKP;  // K padded to 16 (row stride of the T / dT staging buffer)
   // column-slice training kernel (tr_spectral_slice.hip) for the shapes it covers (config 5)
   int sl;                       // 1: SPEC_TRAIN runs k_spec_slice
-  int slSp;                     // its GEMMs: 0 f32 MFMA; bf16 split with X in two pieces: 1 lin packed, 2 not; X in three: 3, 4
+  int slSp;                     // its GEMMs: 0 f32 MFMA; bf16 split with X in two pieces: 1 lin packed, 2 not; X in three: 3, 4;
+                                // signed X (forward X in three pieces, per-sample gradient accumulators): 5, 6
+  int slSpBase, slSigned;       // the plan's form for non-negative X, and whether its signed-X form (+4) runs
   int slDt, sl_Dp;              // rows d >= 128 (<= 2), rows of the phi(A1) / phi(C1) tables
   int sl_oTail, sl_oEx, sl_oTP, sl_oPart, sl_oN1, sl_oLoss, sl_lds_floats;  // LDS carve (floats)
 };
@@ -80,6 +82,7 @@ hipError_t launch_specg(int mode, const SpecGeom& g, int nchunks, const float* X
 // launch (SPEC_TRAIN only; same outputs as launch_spec_fused)
 void spec_slice_geom(SpecGeom* g);
 hipError_t spec_slice_prepare(SpecGeom* g);
+int spec_slice_signed_sp(const SpecGeom& g);  // the slice kernel form for signed X (tr_plan_set_x_range)
 hipError_t launch_spec_slice(const SpecGeom& g, int grid, const float* X, int64_t N, int64_t xld, const float* phi,
                              const float* Phi0, const float* wts, const float* y, float scale, float* slab,
                              int64_t slab_stride, double* dpart, float* out, int64_t rows_per_wg, int reverse,

@@ -57,10 +57,6 @@
 //    lanes, lanes past the Dt tail rows masked by an out-of-range offset) right after the wave's
 //    pieces of the tiles that hold its tail rows (their 128-B lines are then on their way into L2);
 //  - the epilogue's table reads carry no per-element lane masks (see tab8).
-#ifndef TR_SLICE_ACC
-#define TR_SLICE_ACC 0  // EXPERIMENT: 1 gradient products into a zero accumulator per sample, added by VALU;
-                        // 2 the forward's per k step as well
-#endif
 #ifndef TR_SLICE_PROFILE
 #define TR_SLICE_PROFILE 0  // profiling build: per-phase cycle counts of wave 0 of workgroups 0..255
 #endif
@@ -241,12 +237,25 @@ __device__ __forceinline__ sl_f4 sl_mfma_lp(const sl_u4 (&a)[3], const sl_u4 (&b
 }
 // SP (the kernel's GEMM form): 0 f32 MFMA; 1 / 2 bf16 split with a two-piece X, lin columns
 // packed (Rn <= 8) / not; 3 / 4 the same with the three-piece X
-#define SL_LP(SP) ((SP) == 1 || (SP) == 3)
-#define SL_XP(SP) ((SP) >= 3 ? 3 : 2)
-#ifndef TR_SLICE_FWD3
-#define TR_SLICE_FWD3 0  // EXPERIMENT: the forward's X in three pieces whatever SP says
+// SP 5 / 6 (signed X, the plan's choice from X's range, tr_plan_set_x_range): the forward's X in
+// three pieces (T = X Phi0 cancels on signed samples, and the norms of T amplify its error) and
+// the gradient's in two.  Forms 3-6 (with tail rows) form the gradient GEMM's products of each
+// sample in a zero accumulator, added to the launch-long one by a VALU add: the bf16 MFMA's
+// accumulation truncates small addends toward the accumulator, a sign-dependent bias over a
+// workgroup's 128 samples.  Measured at full config-5 size against fp64 (worst gradient, signed X
+// / |X|; gpurun_out/r06a, r06b): SP 1 2.8e-6 / 3.5e-7; forward three-piece alone 1.6e-6; SP 5
+// 8.6e-7 / 9.4e-8; SP 3 with the accumulators 5.5e-7 / 8.2e-8 (without: 1.8e-6 / 3.3e-7); the
+// reference's own fp32 2.4e-6 / 2.1e-6.  Kernel time at c5: SP 5 +13 %, SP 3 +20 % over SP 1;
+// |X| (spectral magnitudes, bench.py c5) keeps SP 1.
+#ifndef TR_SLICE_ACCUM
+#define TR_SLICE_ACCUM 1  // 0: no per-sample accumulators (the negative-control build, Makefile negctl)
 #endif
-#define SL_XPF(SP) (TR_SLICE_FWD3 ? 3 : SL_XP(SP))
+#define SL_LP(SP) ((SP) == 1 || (SP) == 3 || (SP) == 5)
+#define SL_XP(SP) ((SP) == 3 || (SP) == 4 ? 3 : 2)   // gradient GEMM
+#define SL_XPF(SP) ((SP) >= 3 ? 3 : 2)               // forward GEMM
+// per-sample gradient accumulators: forms 3-6 with tail rows (without them, D <= 128, the
+// accumulator temporaries push the kernel past 256 VGPRs into scratch)
+#define SL_ACC(SP, DT) (TR_SLICE_ACCUM && (SP) >= 3 && (DT) > 0)
 template <int CTRL>
 __device__ __forceinline__ float sl_dpp(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
@@ -624,18 +633,6 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
           }
           if ((q & 1) && !(TR_SLICE_SKIP & 2)) {
             const int S = q >> 1;
-            if (TR_SLICE_ACC & 2) {
-              const sl_f4 z = {0.f, 0.f, 0.f, 0.f};
-              T00 += sl_mfma6<SL_XPF(SP)>(xf[0], bs[S], z);
-              T01 += sl_mfma6<SL_XPF(SP)>(xf[1], bs[S], z);
-              if constexpr (SL_LP(SP)) {
-                T10 += sl_mfma_lp<SL_XPF(SP)>(xf[0], bl[S], z);
-                T11 += sl_mfma_lp<SL_XPF(SP)>(xf[1], bl[S], z);
-              } else {
-                T10 += sl_mfma6<SL_XPF(SP)>(xf[0], bl[S], z);
-                T11 += sl_mfma6<SL_XPF(SP)>(xf[1], bl[S], z);
-              }
-            } else {
             T00 = sl_mfma6<SL_XPF(SP)>(xf[0], bs[S], T00);
             T01 = sl_mfma6<SL_XPF(SP)>(xf[1], bs[S], T01);
             if constexpr (SL_LP(SP)) {
@@ -644,7 +641,6 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
             } else {
               T10 = sl_mfma6<SL_XPF(SP)>(xf[0], bl[S], T10);
               T11 = sl_mfma6<SL_XPF(SP)>(xf[1], bl[S], T11);
-            }
             }
           }
         }
@@ -969,7 +965,7 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
               if (q + 1 < ntl) dma_piece(nn, q + 1, 0);
             }
             if (!(TR_SLICE_SKIP & 4)) {
-              if (TR_SLICE_ACC & 1)
+              if constexpr (SL_ACC(SP, DT))
                 gacc[q][0] += sl_mfma6<SL_XP(SP)>(af, ds, sl_f4{0.f, 0.f, 0.f, 0.f});
               else
                 gacc[q][0] = sl_mfma6<SL_XP(SP)>(af, ds, gacc[q][0]);
@@ -979,13 +975,13 @@ __global__ __launch_bounds__(SL_T) void k_spec_slice(
               if (TAIL_LAST && Dt > 0 && q + 1 == qt) dma_tail(nn);
             }
             if (!(TR_SLICE_SKIP & 4)) {
-              const sl_f4 c1 = (TR_SLICE_ACC & 1) ? sl_f4{0.f, 0.f, 0.f, 0.f} : gacc[q][1];
+              const sl_f4 c1 = SL_ACC(SP, DT) ? sl_f4{0.f, 0.f, 0.f, 0.f} : gacc[q][1];
               sl_f4 r1;
               if constexpr (SL_LP(SP))
                 r1 = sl_mfma_lp<SL_XP(SP)>(af, dl, c1);
               else
                 r1 = sl_mfma6<SL_XP(SP)>(af, dl, c1);
-              gacc[q][1] = (TR_SLICE_ACC & 1) ? gacc[q][1] + r1 : r1;
+              gacc[q][1] = SL_ACC(SP, DT) ? gacc[q][1] + r1 : r1;
             }
           }
           if (Dt > 0 && q / TQ == p) {
@@ -1128,19 +1124,43 @@ static const void* slice_kernel(int cc, int dt, int sp) {
     case 1: return slice_kernel_sp<1>(cc, dt);
     case 2: return slice_kernel_sp<2>(cc, dt);
     case 3: return slice_kernel_sp<3>(cc, dt);
-    default: return slice_kernel_sp<4>(cc, dt);
+    case 4: return slice_kernel_sp<4>(cc, dt);
+    case 5: return slice_kernel_sp<5>(cc, dt);
+    default: return slice_kernel_sp<6>(cc, dt);
   }
 }
 
-hipError_t spec_slice_prepare(SpecGeom* g) {
-  if (!g->sl) return hipSuccess;
-  const void* k = slice_kernel(g->Cc, g->slDt, g->slSp);
-  hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, g->sl_lds_floats * 4);
+static hipError_t slice_runs(const SpecGeom& g, int sp, bool* ok) {
+  const void* k = slice_kernel(g.Cc, g.slDt, sp);
+  hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, g.sl_lds_floats * 4);
   if (e != hipSuccess) return e;
   int per_cu = 0;
-  e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, SL_T, (size_t)g->sl_lds_floats * 4);
+  e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, SL_T, (size_t)g.sl_lds_floats * 4);
   if (e != hipSuccess) return e;
-  if (per_cu < 1) g->sl = 0;  // falls back to k_spec_fused
+  *ok = per_cu >= 1;
+  return hipSuccess;
+}
+
+int spec_slice_signed_sp(const SpecGeom& g) { return g.slSpBase + (g.slDt == 0 ? 2 : 4); }
+
+hipError_t spec_slice_prepare(SpecGeom* g) {
+  g->slSpBase = g->slSp;
+  g->slSigned = 0;
+  if (!g->sl) return hipSuccess;
+  bool ok = false;
+  hipError_t e = slice_runs(*g, g->slSp, &ok);
+  if (e != hipSuccess) return e;
+  if (!ok) {
+    g->sl = 0;  // falls back to k_spec_fused
+    return hipSuccess;
+  }
+  // the signed-X form of a two-piece split (tr_plan_set_x_range picks it per X): SP + 4; without
+  // tail rows (D <= 128) that instantiation spills, and the three-piece form (SP + 2) runs instead
+  if (g->slSp == 1 || g->slSp == 2) {
+    e = slice_runs(*g, spec_slice_signed_sp(*g), &ok);
+    if (e != hipSuccess) return e;
+    g->slSigned = ok ? 1 : 0;
+  }
   return hipSuccess;
 }
 

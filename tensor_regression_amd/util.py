@@ -140,14 +140,18 @@ class HostStream:
         return self.shape[0]
 
     def range(self):
-        """(max |x|, mean x^2) of the host X, computed once (the plan's X-form choice for the
-        multinomial split body, Plan._x_form; the chunks are not measured one by one)."""
+        """(max |x|, the smallest mean x^2 of a nonzero sample, min x) of the host X, computed once
+        (the plan's X-form choice for its split kernels, Plan._x_form; the chunks are not measured
+        one by one)."""
         if getattr(self, "_range", None) is None:
-            a = self.X.reshape(-1)
-            mx = float(a.abs().max()) if a.numel() else 0.0
-            if bool(torch.isnan(a).any()):
-                mx = float("nan")
-            self._range = (mx, float(a.double().square().mean()) if a.numel() else 0.0)
+            a = self.X.reshape(self.shape[0], -1)
+            if a.numel() == 0:
+                self._range = (0.0, float("inf"), 0.0)
+            else:
+                mx = float("nan") if bool(torch.isnan(a).any()) else float(a.abs().max())
+                ms = a.double().square().mean(dim=1)
+                ms = ms[ms > 0]
+                self._range = (mx, float(ms.min()) if ms.numel() else float("inf"), float(a.min()))
         return self._range
 
     @property

@@ -34,5 +34,22 @@ for signed in (False, True):
         worst = max(e[f"grad{f}"] for f in range(6))
         print(json.dumps({"lib": os.path.basename(os.environ.get("TR_HIP_LIB", "libtr_hip.so")), "signed": signed,
                           "form": form, "worst_grad": worst, "errs": e, "describe": d}), flush=True)
+    # the default form's pass time on this X (loss_grad: the slice kernel + its reduction), 30 calls
+    torch.manual_seed(1)
+    m1 = SP.CP_linear_regression(X.shape, y.shape, rank_normal=8, rank_spectral=8, n_complex_dim=1, device=DEV)
+    plan = m1._get_plan(X, N)
+    arena = plan.pack(m1.Bcp_n, m1.Bcp_c, m1.bias)
+    w = torch.ones(16, device=DEV)
+    grad = torch.zeros(plan.num_grads, device=DEV)
+    for _ in range(20):
+        plan.loss_grad(X, y, None, float(N * O), arena, w, grad)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(30):
+        plan.loss_grad(X, y, None, float(N * O), arena, w, grad)
+    e1.record()
+    e1.synchronize()
+    print(json.dumps({"signed": signed, "loss_grad_ms": e0.elapsed_time(e1) / 30, "describe": plan.describe}),
+          flush=True)
     del X, y
     torch.cuda.empty_cache()
