@@ -54,6 +54,9 @@ struct MnlGeom {
   int du_ns;  // split body: samples in the LDS ring (2; 3 at NW = 5, 6)
   int du_pad;  // split body: g.I x g.J fills only part of the compiled (32 NW or 16 NW) x du_jt sample
   int du_jt;   // the duo family's compiled row width (J, or 64 / 128 above a padded J)
+  // split body's row blocks per sample (1; a sample of du_nb * 32 NW (J <= 64) or du_nb * 16 NW rows
+  // streams through the ring one row block per slot) and the LDS offset of the earlier blocks' T / dPhi0
+  int du_nb, bs_oTB;
   // k_mnl_fused fits this shape (mnl_geom_init may accept a shape only the split body runs)
   int fused_ok;
 };

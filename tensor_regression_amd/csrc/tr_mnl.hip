@@ -646,7 +646,7 @@ bool mnl_geom_init(MnlGeom* g, int64_t I, int64_t J, int R, int C, std::string* 
   if (R < 1 || R > kMnlRMax) return no("rank outside [1, 32]");
   if (C < 1 || C > kMnlCMax) return no("classes outside [1, 16]");
   if (I < 1 || J < 4 || J % 4 != 0) return no("second feature dim must be a multiple of 4");
-  if (I * J * 4 > 64 * 1024) return no("sample larger than 64 KiB");
+  if (I * J > (int64_t)1 << 28) return no("sample larger than 1 GiB");
   g->I = (int)I;
   g->J = (int)J;
   g->R = R;
@@ -663,9 +663,11 @@ bool mnl_geom_init(MnlGeom* g, int64_t I, int64_t J, int R, int C, std::string* 
   g->nunits = 2 * g->nA;
   g->fused_ok = 1;
   auto no_fused = [&](const char* m) {
-    if (why) *why = m;
+    if (why && g->fused_ok) *why = m;
     g->fused_ok = 0;
   };
+  // (samples above 64 KiB: only the split body's row-block form, tr_mnl_duo.hip, streams them)
+  if (I * J * 4 > 64 * 1024) no_fused("sample larger than 64 KiB");
   if (g->nunits > MN_NW) no_fused("more than 8 GEMM units (I, J or R too large)");
   g->upw = 1;
   g->nsets = g->nib * g->njb;

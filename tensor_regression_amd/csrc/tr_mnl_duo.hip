@@ -43,6 +43,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <type_traits>
+#include <utility>
 
 #include "tr_common.h"
 #include "tr_mnl.h"
@@ -51,7 +52,7 @@
 #define TR_DUO_PROFILE 0  // profiling build only: per-phase cycle counts of every wave (tools/duo_profile.py)
 #endif
 #if TR_DUO_PROFILE
-__device__ unsigned long long g_duo_prof[512][4][4];
+__device__ unsigned long long g_duo_prof[512][8][4];  // [workgroup][wave][phase]
 #define TR_DUO_MARK(ph)                                           \
   do {                                                            \
     const unsigned long long _now = __builtin_readcyclecounter(); \
@@ -559,7 +560,12 @@ __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, cons
 // wave's i k-step, and dPhi1 = sum_n Wv_n V_n is linear in it: the waves' partials are summed
 // once, at the end.  Every wave runs the softmax epilogue of the previous sample (staged between
 // its GEMM steps) for all 8 ranks; wave 0 alone accumulates dPhiC and the loss.
-template <int JT, int NW, int NS, bool PAD, bool EXACT>
+template <int... T, class F>
+__device__ __forceinline__ void for_each_ic(std::integer_sequence<int, T...>, F&& f) {
+  (f(std::integral_constant<int, T>()), ...);
+}
+
+template <int JT, int NW, int NS, bool PAD, bool EXACT, int NB>
 __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, const int64_t* __restrict__ lab,
                                          const float* __restrict__ class_w, float* lds, const int wv, const int lane) {
   const int t = threadIdx.x;
@@ -573,7 +579,15 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
   const int R = g.R, C = g.C;
   // PAD: the sample's g.I x g.J (g.J % 4 == 0) fills only part of the compiled I x J; the padding
   // rows and column chunks read the sample's first chunk (valid memory) and meet zero Phi0 / Phi1 rows
-  const int Ir = PAD ? g.I : I, Jr = PAD ? g.J : J;
+  // NB > 1 (BLK): a sample of NB * I rows streams through the ring as NB row blocks of I rows, each
+  // one ring slot; T, its U partial and the dPhi0 rows are per block, V accumulates over the blocks,
+  // and the epilogue runs once per sample (no row padding there: g.I = NB * I).  NB is compiled in:
+  // with the block index a run-time value, the block-dependent choices (epilogue or not, V carried
+  // or folded) cost ~300 VALU per block in selects and moves (profiled: 25 % slower per block)
+  constexpr bool BLK = NB > 1;
+  constexpr int nb = NB;
+  static_assert(!BLK || NS == 2, "row blocks: a ring of two");
+  const int Ir = (PAD && !BLK) ? g.I : I, Jr = PAD ? g.J : J;
   // NS = 3: a ring of three samples (the DMA of sample k + 2 goes into the slot of k - 1 while k
   // is computed: two samples in flight), where three fit the workgroup's LDS share
   static_assert(NS == 2 || NS == 3, "ring of two or three slots");
@@ -587,12 +601,6 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
   const bool cok = c < C;
   const float cwl = cok ? class_w[c] : 0.f;
   const float NEG = -__builtin_huge_valf();
-  float gsel[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) gsel[q] = gq == q ? 1.f : 0.f;
-  float rsel[8];  // 1 where this lane's accumulator rank (n & 7) == r
-#pragma unroll
-  for (int r = 0; r < 8; ++r) rsel[r] = r8 == r ? 1.f : 0.f;
 
   const int it0 = NT == 2 ? 32 * wv : 16 * wv;                    // first T row of this wave
   const int iv0 = JT == 64 ? 32 * wv : 32 * (wv % NKS);           // V k-step (rows) of this wave
@@ -621,29 +629,74 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
       bsplit((rok && (!PAD || j < Jr)) ? P1[(int64_t)j * R + r8] : 0.f,
              (rok && (!PAD || j + 1 < Jr)) ? P1[(int64_t)(j + 1) * R + r8] : 0.f, bT12[s][v], bT3[s][v], hT[s][v]);
     }
+  // V (Phi0, element e <-> i = iv0 + 8 gq + e) and the U weights: T accumulator (lane (n, gq), reg
+  // v) = T[it0 + 16 tt + 4 gq + v][n & 7] after the column fold; lanes n >= 8 hold the same values
+  // and weigh 0.  Both depend on the row block: BLK loads the raw Phi0 values of the next block at
+  // the end of a block (they land with that block's LDS-DMA wait) and splits them after its barrier
+  float pvr[8], phiU[NT][4];
+  // BLK: buffer loads at one per-lane byte offset each for the V and U rows, the block's row as the
+  // scalar offset (64-bit addresses per element, hoisted out of the sample loop, held 32 VGPRs);
+  // lanes whose rank is past R (or whose U weight is unused) point past the buffer and read 0
+  const __amdgpu_buffer_rsrc_t prs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)P0, (short)0, (int)(g.I * R * 4), 0x00020000);
+  const int vo_v = rok ? ((iv0 + 8 * gq) * R + r8) * 4 : 0x40000000;
+  const int vo_u = (lo8 && rok) ? ((it0 + 4 * gq) * R + r8) * 4 : 0x40000000;
+  auto load_rows = [&](int i0, float (&pu)[NT][4]) {
+    if constexpr (BLK) {
 #pragma unroll
-  for (int v = 0; v < 4; ++v) {  // V (Phi0, element e <-> i = iv0 + 8 gq + e)
-    const int i = iv0 + 8 * gq + 2 * v;
-    bsplit((rok && (!PAD || i < Ir)) ? P0[(int64_t)i * R + r8] : 0.f,
-           (rok && (!PAD || i + 1 < Ir)) ? P0[(int64_t)(i + 1) * R + r8] : 0.f, bV12[v], bV3[v], hV[v]);
-  }
-  // U weights: T accumulator (lane (n, gq), reg v) = T[it0 + 16 tt + 4 gq + v][n & 7] after the
-  // column fold; lanes n >= 8 hold the same values and weigh 0
-  float phiU[NT][4];
+      for (int e = 0; e < 8; ++e)
+        pvr[e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(prs, vo_v, (i0 + e) * R * 4, 0));
 #pragma unroll
-  for (int tt = 0; tt < NT; ++tt)
+      for (int tt = 0; tt < NT; ++tt)
 #pragma unroll
-    for (int v = 0; v < 4; ++v)
-      phiU[tt][v] = (lo8 && rok && (!PAD || it0 + 16 * tt + 4 * gq + v < Ir))
-                        ? P0[(int64_t)(it0 + 16 * tt + 4 * gq + v) * R + r8]
-                        : 0.f;
-  // epilogue weights: pc[r] = w_r PhiC[c][r]; row gq's ranks gq, gq + 4
+        for (int v = 0; v < 4; ++v)
+          pu[tt][v] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(prs, vo_u, (i0 + 16 * tt + v) * R * 4, 0));
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int i = iv0 + 8 * gq + e;
+        pvr[e] = (rok && (!PAD || i < Ir)) ? P0[(int64_t)i * R + r8] : 0.f;
+      }
+#pragma unroll
+      for (int tt = 0; tt < NT; ++tt)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int i = it0 + 16 * tt + 4 * gq + v;
+          pu[tt][v] = (lo8 && rok && (!PAD || i < Ir)) ? P0[(int64_t)i * R + r8] : 0.f;
+        }
+    }
+  };
+  auto split_rows = [&]() {
+#pragma unroll
+    for (int v = 0; v < 4; ++v) bsplit(pvr[2 * v], pvr[2 * v + 1], bV12[v], bV3[v], hV[v]);
+    if constexpr (BLK)  // the U weights' loads complete here too, before this block's first LDS-DMA piece
+#pragma unroll
+      for (int tt = 0; tt < NT; ++tt)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) asm volatile("" : "+v"(phiU[tt][v]));
+  };
+  load_rows(0, phiU);
+  if constexpr (!BLK) split_rows();
+  // epilogue weights: pc[r] = w_r PhiC[c][r]; row gq's ranks gq, gq + 4.  BLK reads pc[r] from an
+  // LDS table [class 16][rank 8] (the rank-block body's Z slots, unused here) in the epilogue: the
+  // row-block form needs the 8 registers
   float pc[8];
 #pragma unroll
-  for (int r = 0; r < 8; ++r) pc[r] = (cok && r < R) ? a.w[r] * PC[c * R + r] : 0.f;
-  const float pcg0 = pc[gq & 3], pcg1 = pc[4 + (gq & 3)];
+  for (int r = 0; r < 8; ++r) pc[r] = (!BLK && cok && r < R) ? a.w[r] * PC[c * R + r] : 0.f;
+  auto pc_of = [&](int r) { return (cok && r < R) ? a.w[r] * PC[c * R + r] : 0.f; };
+  const float pcg0 = BLK ? pc_of(gq) : pc[gq & 3], pcg1 = BLK ? pc_of(gq + 4) : pc[4 + (gq & 3)];
+  float* sPC = lds + g.du_oZ;
+  if constexpr (BLK)
+    for (int e = t; e < 128; e += NT_) sPC[e] = (e / 8 < C && e % 8 < R) ? a.w[e % 8] * PC[(e / 8) * R + e % 8] : 0.f;
   const float wg0 = gq < R ? a.w[gq] : 0.f, wg1 = gq + 4 < R ? a.w[gq + 4] : 0.f;
   for (int e = t; e < NS * NW * 8; e += NT_) sU[e] = 0.f;
+  // BLK: the folded T of blocks 0 .. nb - 2 of the previous sample and this wave's dPhi0 rows of
+  // those blocks, [2][nb - 1][NW][NT][gq][rank 8][v 4] (lanes n < 8 only; the last block's in registers)
+  float* sTB = lds + g.bs_oTB;
+  const int tbn = (nb - 1) * NW * NT * 128;
+  auto tb_at = [&](int bb, int tt) { return ((bb * NW + wv) * NT + tt) * 128 + gq * 32 + r8 * 4; };
+  if constexpr (BLK)
+    for (int e = t; e < 2 * tbn; e += NT_) sTB[e] = 0.f;
 
   // LDS-DMA map (as the rank-block form): wave wv issues the 1 KiB groups wv + NW gi of every sample
   uint32_t goff[8];
@@ -698,84 +751,109 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
 
   // ---- epilogue of one sample in 8 stages (duo_body's chain, all 8 ranks: row gq carries ranks
   // gq and gq + 4) ----
-  float uS = 0.f, uR[8];
-#pragma unroll
-  for (int r = 0; r < 8; ++r) uR[r] = 0.f;
-  float e_x = 0.f, e_ez = 0.f, e_sum = 0.f, e_S = 0.f, e_q = 0.f, e_Sq = 0.f, e_Sy = 0.f;
-  float e_s2 = 0.f, e_d1 = 0.f, e_e1 = 0.f, e_dz = 0.f, e_a0 = 0.f, e_b0 = 0.f, e_y0 = 0.f, e_a1 = 0.f, e_b1 = 0.f,
-        e_y1 = 0.f, e_w0 = 0.f, e_w1 = 0.f, e_wv = 0.f;
-  bool e_isy = false;
-  auto epi = [&](int st, int zs, int64_t yE, float cwE) {
+  // (the stages' values, one instance per epilogue: an instance shared across iterations would be
+  // carried around the BLK loop, whose stages run only in a sample's first block)
+  struct EpiSt {
+    float uS, uR[8];
+    float e_x, e_ez, e_sum, e_S, e_q, e_Sq, e_Sy;
+    float e_s2, e_d1, e_e1, e_dz, e_a0, e_b0, e_y0, e_a1, e_b1, e_y1, e_w0, e_w1, e_wv;
+    bool e_isy;
+  };
+  auto epi = [&](EpiSt& E, int st, int zs, int64_t yE, float cwE) {
     if (TR_DUO_SKIP & 4) return;
     if (st == 0) {  // U[r] = sum of the NW waves' partials (lane r), wave order
       const float* pu = sU + zs * (8 * NW) + r8;
-      uS = pu[0];
+      E.uS = pu[0];
 #pragma unroll
-      for (int w = 1; w < NW; ++w) uS += pu[8 * w];
+      for (int w = 1; w < NW; ++w) E.uS += pu[8 * w];
     } else if (st == 1) {
 #pragma unroll
-      for (int r = 0; r < 8; ++r) uR[r] = du_rdl(uS, r);
-      float zz = pc[0] * uR[0];
+      for (int r = 0; r < 8; ++r) E.uR[r] = du_rdl(E.uS, r);
+      float zz;
+      if constexpr (BLK) {
+        const du_f32x4 p0 = *reinterpret_cast<const du_f32x4*>(sPC + 8 * c);
+        const du_f32x4 p1 = *reinterpret_cast<const du_f32x4*>(sPC + 8 * c + 4);
+        zz = p0[0] * E.uR[0];
 #pragma unroll
-      for (int r = 1; r < 8; ++r) zz = fmaf(pc[r], uR[r], zz);
-      zz = cok ? zz : NEG;
-      e_x = zz - du_row_max16(zz);
-    } else if (st == 2) {
-      e_ez = cok ? du_exp(e_x) : 0.f;
-      e_sum = du_row_sum16(e_ez);
-    } else if (st == 3) {
-      e_S = e_ez * __builtin_amdgcn_rcpf(e_sum);
-      e_q = cok ? du_exp(e_S) : 0.f;
-      e_isy = cok && (int64_t)c == yE;
-      e_Sq = e_S * e_q;
-      e_Sy = e_isy ? e_S : 0.f;
-    } else if (st == 4) {
-      e_s2 = du_row_sum16(e_q);
-      e_d1 = du_row_sum16(e_Sq);
-      e_e1 = du_row_sum16(e_Sy);
-      e_a0 = du_row_sum16(e_Sq * pcg0);
-      e_b0 = du_row_sum16(e_S * pcg0);
-      e_y0 = du_row_sum16(e_Sy * pcg0);
-      e_a1 = du_row_sum16(e_Sq * pcg1);
-      e_b1 = du_row_sum16(e_S * pcg1);
-      e_y1 = du_row_sum16(e_Sy * pcg1);
-    } else if (st == 5) {
-      const float is2 = __builtin_amdgcn_rcpf(e_s2);
-      const float kk = cwE * a.scale;
-      const float dot = kk * (e_d1 * is2 - e_e1);
-      lsum += (wv == 0 && lane == 0) ? (double)cwE * (double)(du_log(e_s2) - e_e1) : 0.0;
-      const float dS = cok ? kk * (e_q * is2 - (e_isy ? 1.0f : 0.0f)) : 0.f;
-      e_dz = cok ? e_S * (dS - dot) : 0.f;
-      e_w0 = kk * (e_a0 * is2 - e_y0) - dot * e_b0;  // Wv[gq]
-      e_w1 = kk * (e_a1 * is2 - e_y1) - dot * e_b1;  // Wv[gq + 4]
-    } else if (st == 6) {
-      // Wv[r] of this lane's accumulator rank r = n & 7 (rank r < 4: row r's e_w0, else row r - 4's e_w1)
-      float wv8 = 0.f;
+        for (int r = 1; r < 8; ++r) zz = fmaf(r < 4 ? p0[r] : p1[r - 4], E.uR[r], zz);
+      } else {
+        zz = pc[0] * E.uR[0];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        wv8 = fmaf(du_rdl(e_w0, 16 * r), rsel[r], wv8);
-        wv8 = fmaf(du_rdl(e_w1, 16 * r), rsel[r + 4], wv8);
+        for (int r = 1; r < 8; ++r) zz = fmaf(pc[r], E.uR[r], zz);
       }
-      e_wv = wv8;
+      zz = cok ? zz : NEG;
+      E.e_x = zz - du_row_max16(zz);
+    } else if (st == 2) {
+      E.e_ez = cok ? du_exp(E.e_x) : 0.f;
+      E.e_sum = du_row_sum16(E.e_ez);
+    } else if (st == 3) {
+      E.e_S = E.e_ez * __builtin_amdgcn_rcpf(E.e_sum);
+      E.e_q = cok ? du_exp(E.e_S) : 0.f;
+      E.e_isy = cok && (int64_t)c == yE;
+      E.e_Sq = E.e_S * E.e_q;
+      E.e_Sy = E.e_isy ? E.e_S : 0.f;
+    } else if (st == 4) {
+      E.e_s2 = du_row_sum16(E.e_q);
+      E.e_d1 = du_row_sum16(E.e_Sq);
+      E.e_e1 = du_row_sum16(E.e_Sy);
+      E.e_a0 = du_row_sum16(E.e_Sq * pcg0);
+      E.e_b0 = du_row_sum16(E.e_S * pcg0);
+      E.e_y0 = du_row_sum16(E.e_Sy * pcg0);
+      E.e_a1 = du_row_sum16(E.e_Sq * pcg1);
+      E.e_b1 = du_row_sum16(E.e_S * pcg1);
+      E.e_y1 = du_row_sum16(E.e_Sy * pcg1);
+    } else if (st == 5) {
+      const float is2 = __builtin_amdgcn_rcpf(E.e_s2);
+      const float kk = cwE * a.scale;
+      const float dot = kk * (E.e_d1 * is2 - E.e_e1);
+      lsum += (wv == 0 && lane == 0) ? (double)cwE * (double)(du_log(E.e_s2) - E.e_e1) : 0.0;
+      const float dS = cok ? kk * (E.e_q * is2 - (E.e_isy ? 1.0f : 0.0f)) : 0.f;
+      E.e_dz = cok ? E.e_S * (dS - dot) : 0.f;
+      E.e_w0 = kk * (E.e_a0 * is2 - E.e_y0) - dot * E.e_b0;  // Wv[gq]
+      E.e_w1 = kk * (E.e_a1 * is2 - E.e_y1) - dot * E.e_b1;  // Wv[gq + 4]
+    } else if (st == 6) {
+      // Wv[r] of this lane's accumulator rank r = n & 7 (rank r < 4: row r's e_w0, else row r - 4's
+      // e_w1), fetched from lane 16 (r & 3)
+      const int src = 64 * (r8 & 3);
+      const float w0 = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(E.e_w0)));
+      const float w1 = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(E.e_w1)));
+      E.e_wv = r8 < 4 ? w0 : w1;
     } else {
 #pragma unroll
-      for (int q = 0; q < NT; ++q) gT[q] += e_wv * TP[q];
+      for (int q = 0; q < NT; ++q) gT[q] += E.e_wv * TP[q];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) gV[q] += e_wv * VP[q];
+      for (int q = 0; q < 4; ++q) gV[q] += E.e_wv * VP[q];
+      if constexpr (BLK) {
+        if (lo8)
+#pragma unroll
+          for (int bb = 0; bb < nb - 1; ++bb)
+#pragma unroll
+            for (int tt = 0; tt < NT; ++tt) {
+              const du_f32x4 tp = *reinterpret_cast<const du_f32x4*>(sTB + tb_at(bb, tt));
+              du_f32x4* gp = reinterpret_cast<du_f32x4*>(sTB + tbn + tb_at(bb, tt));
+              *gp += E.e_wv * tp;
+            }
+      }
       if (wv == 0) {  // dPhiC[c][r] += dZ[c] w_r U[r], r = gq, gq + 4
-        const float u0 = fmaf(uR[3], gsel[3], fmaf(uR[2], gsel[2], fmaf(uR[1], gsel[1], uR[0] * gsel[0])));
-        const float u1 = fmaf(uR[7], gsel[3], fmaf(uR[6], gsel[2], fmaf(uR[5], gsel[1], uR[4] * gsel[0])));
-        dpc0 = fmaf(e_dz, wg0 * u0, dpc0);
-        dpc1 = fmaf(e_dz, wg1 * u1, dpc1);
+        const float u0 = __int_as_float(__builtin_amdgcn_ds_bpermute(4 * gq, __float_as_int(E.uS)));  // U[gq]
+        const float u1 = __int_as_float(__builtin_amdgcn_ds_bpermute(4 * gq + 16, __float_as_int(E.uS)));  // U[gq + 4]
+        dpc0 = fmaf(E.e_dz, wg0 * u0, dpc0);
+        dpc1 = fmaf(E.e_dz, wg1 * u1, dpc1);
       }
     }
   };
 
   auto dma_piece = [&](uint32_t off, const float* src, uint32_t m0v) { du_dma_s(off, src, m0v); };
+  // at NW = 8 (unpadded) a wave's group gi starts 16 (J = 128) or 32 (J = 64) rows after its group 0,
+  // with the same chunk swizzle: one per-lane offset and 8 KiB more of scalar base per group (seven
+  // VGPRs fewer)
+  constexpr bool GAFF = NW == 8 && !PAD;
+  auto goff_of = [&](int gi) { return GAFF ? goff[0] : goff[gi]; };
+  auto src_of_group = [&](const float* p, int gi) { return GAFF ? p + 2048 * gi : p; };
   auto dma_sample = [&](const float* src, int slot) {
 #pragma unroll
     for (int gi = 0; gi < 8; ++gi)
-      dma_piece(goff[gi], src, lbase + (uint32_t)(slot * 4 * SPF) + (uint32_t)(wv + NW * gi) * 1024u);
+      dma_piece(goff_of(gi), src_of_group(src, gi), lbase + (uint32_t)(slot * 4 * SPF) + (uint32_t)(wv + NW * gi) * 1024u);
   };
   // the kernel is bound by the bytes in flight per CU, not by its issue stream (no-LDS-DMA
   // ablation: 0.256 vs 0.368 ms at c3): a ring of three keeps two samples in flight
@@ -787,11 +865,28 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
   unsigned long long prof_t = __builtin_readcyclecounter();
 #endif
 
-  auto iter = [&](auto slot_c, int k) {
+  // BLK: the current sample's label and class weight (set at its first block) and this wave's U
+  // partial, carried over the sample's blocks; its V partial is carried in VP, which is free once
+  // the first block's epilogue stage 7 has consumed the previous sample's
+  int64_t yB = 0;
+  float cwB = 0.f, uacc = 0.f;
+  // (!BLK: k is the sample and b = 0; BLK: block b of sample k, ring slot = block-iteration parity)
+  auto iter = [&](auto slot_c, int k, auto b_c) {
     constexpr int SL = decltype(slot_c)::value;
-    const int64_t yC = yN;
-    const bool more = k + 1 < nr;
-    if (!(TR_DUO_SKIP & 16)) yN = lab[sample_of(more ? k + 1 : k)];
+    constexpr int b = decltype(b_c)::value;
+    constexpr bool bfirst = b == 0, blast = b == nb - 1;
+    int64_t yC;
+    if constexpr (BLK) {
+      if (bfirst) {
+        yB = yN;
+        if (!(TR_DUO_SKIP & 16)) yN = lab[sample_of(k + 1 < nr ? k + 1 : k)];
+      }
+      yC = yB;
+    } else {
+      yC = yN;
+      const bool more = k + 1 < nr;
+      if (!(TR_DUO_SKIP & 16)) yN = lab[sample_of(more ? k + 1 : k)];
+    }
     if (NS == 3)
       asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // own pieces of k (those of k + 1 may be in flight)
     else
@@ -799,13 +894,29 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
     TR_DUO_MARK(0);
     du_barrier();  // everyone's pieces of k; U partials of k - 1
     TR_DUO_MARK(1);
-    const float cwC = du_rdl(cwl, (int)yC);
+    float cwC;
+    if constexpr (BLK) {
+      if (bfirst) cwB = du_rdl(cwl, (int)yC);
+      cwC = cwB;
+      split_rows();  // this block's Phi0 operands (loaded at the end of the previous block)
+    } else {
+      cwC = du_rdl(cwl, (int)yC);
+    }
     // sample k + 2 into this slot once it is read (past the end: a harmless refill of a valid sample)
     const int kd = k + NS - 1;  // the sample this iteration's DMA brings in
     constexpr int PS = (SL + NS - 1) % NS;     // slot of sample k - 1 (and of the DMA's target)
-    const float* psrc = (kd < nr && !(TR_DUO_SKIP & 1)) ? src_of(kd) : src_of(nr - 1);
+    const float* psrc;
+    if constexpr (BLK) {  // the next block (of this sample or the next), or this one again past the end
+      const float* cur = src_of(k) + (int64_t)b * I * Jr;
+      psrc = (TR_DUO_SKIP & 1) ? cur : b + 1 < nb ? cur + (int64_t)I * Jr : k + 1 < nr ? src_of(k + 1) : cur;
+    } else {
+      psrc = (kd < nr && !(TR_DUO_SKIP & 1)) ? src_of(kd) : src_of(nr - 1);
+    }
     const uint32_t pm0 = lbase + (uint32_t)(PS * 4 * SPF) + (uint32_t)wv * 1024u;
-    epi(0, PS, yP, cwP);
+    // U partial slots: per ring slot (!BLK), per sample parity (BLK)
+    const int zsP = BLK ? ((k - 1) & 1) : PS, zsC = BLK ? (k & 1) : SL;
+    EpiSt E;
+    if constexpr (bfirst) epi(E, 0, zsP, yP, cwP);
     const float* sb = lds + SL * SPF;
     du_f32x4 aT[NT], aV[4];
 #pragma unroll
@@ -826,7 +937,7 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
     }
 #pragma unroll
     for (int st = 0; st < NU + 4; ++st) {
-      if (!(TR_DUO_SKIP & 8)) dma_piece(goff[st], psrc, pm0 + (uint32_t)st * (uint32_t)(NW * 1024));
+      if (!(TR_DUO_SKIP & 8)) dma_piece(goff_of(st), src_of_group(psrc, st), pm0 + (uint32_t)st * (uint32_t)(NW * 1024));
       sl_u4 x1, x2, x3;  // the k step's X pieces (pairs per VGPR)
       auto split = [&](float e0, float e1, int v) {
         if constexpr (EXACT) {
@@ -866,12 +977,12 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
         for (int v = 0; v < 4; ++v) split(xv[2 * v][tv], xv[2 * v + 1][tv], v);
         gemm(aV[tv], bV12, bV3, hV);
       }
-      if (st >= 1 && st <= 7) epi(st, PS, yP, cwP);
+      if (bfirst && st >= 1 && st <= 7) epi(E, st, zsP, yP, cwP);  // (bfirst, st: compile-time)
       __builtin_amdgcn_sched_barrier(0);
     }
     TR_DUO_MARK(2);
     // fold the piece columns (rank r = column r + column r + 8), U partial of this wave -> LDS
-    float u = 0.f;
+    float u = BLK ? uacc : 0.f;
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) {
 #pragma unroll
@@ -879,24 +990,58 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
         aT[tt][v] += du_dpp<0x128>(aT[tt][v]);  // row_ror:8
         u = fmaf(phiU[tt][v], aT[tt][v], u);
       }
-      TP[tt] = aT[tt];
+      if (blast) {
+        TP[tt] = aT[tt];
+      } else if (lo8) {  // (BLK) block b's T until the sample's epilogue
+        *reinterpret_cast<du_f32x4*>(sTB + tb_at(b, tt)) = aT[tt];
+      }
     }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-#pragma unroll
-      for (int v = 0; v < 4; ++v) aV[q][v] += du_dpp<0x128>(aV[q][v]);
-      VP[q] = aV[q];
+    if constexpr (BLK) {
+      uacc = blast ? 0.f : u;
+      // the next block's Phi0 rows (issuing them at the first V step instead, with the U weights
+      // double-buffered, measured no faster)
+      load_rows(b + 1 < nb ? (b + 1) * I : 0, phiU);
     }
-    u = du_xor32_sum(du_xor16_sum(u));  // lane (n < 8, any row): this wave's U partial of rank n
-    if (lane < 8) sU[SL * (8 * NW) + wv * 8 + lane] = u;
-    yP = yC;
-    cwP = cwC;
+    if constexpr (BLK) {  // V over the blocks (folded at the last)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) aV[q] = bfirst ? aV[q] : VP[q] + aV[q];
+      if (!blast)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) VP[q] = aV[q];
+    }
+    if (blast) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+#pragma unroll
+        for (int v = 0; v < 4; ++v) aV[q][v] += du_dpp<0x128>(aV[q][v]);
+        VP[q] = aV[q];
+      }
+      u = du_xor32_sum(du_xor16_sum(u));  // lane (n < 8, any row): this wave's U partial of rank n
+      if (lane < 8) sU[zsC * (8 * NW) + wv * 8 + lane] = u;
+      yP = yC;
+      cwP = cwC;
+    }
     TR_DUO_MARK(3);
+    if constexpr (BLK) __builtin_amdgcn_sched_barrier(0);  // (no scheduling across the block boundary)
   };
-  for (int k = 0; k < nr; k += NS) {
-    iter(std::integral_constant<int, 0>(), k);
-    if (k + 1 < nr) iter(std::integral_constant<int, 1>(), k + 1);
-    if (NS == 3 && k + 2 < nr) iter(std::integral_constant<int, NS == 3 ? 2 : 0>(), k + 2);
+  using B0 = std::integral_constant<int, 0>;
+  if constexpr (BLK) {
+    // one trip: the blocks of one sample (NB even) or of two (NB odd), so that every block's ring
+    // slot (block-iteration parity) is a compile-time constant
+    constexpr int TRIP = NB % 2 == 0 ? NB : 2 * NB;
+    for (int k = 0; k < nr; k += TRIP / NB) {
+      for_each_ic(std::make_integer_sequence<int, TRIP>(), [&](auto t_c) {
+        constexpr int t = decltype(t_c)::value;
+        if (TRIP == NB || k + t / NB < nr)
+          iter(std::integral_constant<int, t % 2>(), k + t / NB, std::integral_constant<int, t % NB>());
+      });
+    }
+  } else {
+    for (int k = 0; k < nr; k += NS) {
+      iter(std::integral_constant<int, 0>(), k, B0());
+      if (k + 1 < nr) iter(std::integral_constant<int, 1>(), k + 1, B0());
+      if (NS == 3 && k + 2 < nr) iter(std::integral_constant<int, NS == 3 ? 2 : 0>(), k + 2, B0());
+    }
   }
 #if TR_DUO_PROFILE
   if (lane == 0 && blockIdx.x < 512)
@@ -905,8 +1050,9 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last (harmless) refill has landed
   du_barrier();  // U partials of the last sample
   if (nr > 0) {
+    EpiSt E;
 #pragma unroll
-    for (int st = 0; st < 8; ++st) epi(st, (nr - 1) % NS, yP, cwP);
+    for (int st = 0; st < 8; ++st) epi(E, st, BLK ? (nr - 1) & 1 : (nr - 1) % NS, yP, cwP);
   }
 
   // ---- fixed-order reduction into an LDS image of the arena (wave order), slab ----
@@ -916,11 +1062,21 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
   __syncthreads();
   for (int ws = 0; ws < NW; ++ws) {
     if (ws == wv && lo8 && rok) {
+      const int ib = BLK ? (nb - 1) * I : 0;  // BLK: the register rows are the last block's
 #pragma unroll
       for (int tt = 0; tt < NT; ++tt)
 #pragma unroll
         for (int v = 0; v < 4; ++v)
-          if (!PAD || it0 + 16 * tt + 4 * gq + v < g.I) sG[(it0 + 16 * tt + 4 * gq + v) * R + r8] += gT[tt][v];
+          if (!PAD || BLK || it0 + 16 * tt + 4 * gq + v < g.I) sG[(ib + it0 + 16 * tt + 4 * gq + v) * R + r8] += gT[tt][v];
+      if constexpr (BLK)
+#pragma unroll
+        for (int bb = 0; bb < nb - 1; ++bb)
+#pragma unroll
+          for (int tt = 0; tt < NT; ++tt) {
+            const du_f32x4 gt = *reinterpret_cast<const du_f32x4*>(sTB + tbn + tb_at(bb, tt));
+#pragma unroll
+            for (int v = 0; v < 4; ++v) sG[(bb * I + it0 + 16 * tt + 4 * gq + v) * R + r8] += gt[v];
+          }
 #pragma unroll
       for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -948,7 +1104,7 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
 
 // NW waves per workgroup, 8 / NW workgroups per CU (the second bound is waves per SIMD: two,
 // 256 VGPRs each), a ring of NS samples
-template <int JT, int NW, int NS, bool PAD, bool EXACT>
+template <int JT, int NW, int NS, bool PAD, bool EXACT, int NB>
 __global__ __launch_bounds__(NW * TR_WAVE, 2) void k_mnl_bsp(MnlGeom g, DuArgs a, const int64_t* __restrict__ lab,
                                                                const float* __restrict__ class_w,
                                                                const int32_t* __restrict__ stop) {
@@ -956,7 +1112,7 @@ __global__ __launch_bounds__(NW * TR_WAVE, 2) void k_mnl_bsp(MnlGeom g, DuArgs a
   if (stop != nullptr && *stop != 0) return;
   const int lane = threadIdx.x & (TR_WAVE - 1);
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / TR_WAVE);
-  bsp_body<JT, NW, NS, PAD, EXACT>(g, a, lab, class_w, lds, wv, lane);
+  bsp_body<JT, NW, NS, PAD, EXACT, NB>(g, a, lab, class_w, lds, wv, lane);
 }
 
 template <int JT>
@@ -977,18 +1133,35 @@ __global__ __launch_bounds__(DU_T, 2) void k_mnl_duo(MnlGeom g, DuArgs a, const 
 #define TR_BSP_LIST(X) \
   X(64, 2, 2) X(64, 3, 2) X(64, 4, 2) X(64, 5, 2) X(64, 5, 3) X(64, 6, 2) X(64, 6, 3) X(64, 7, 2) \
   X(64, 8, 2) X(128, 4, 2) X(128, 6, 2) X(128, 6, 3) X(128, 8, 2)
+// ... and its row-block instantiations (J, NW, ring slots, blocks): samples of NB blocks of 32 NW x
+// 64 or 16 NW x 128 rows.  (At (64, 8) only two blocks fit the LDS; (128, 8) with three and every
+// four-block form spill: such samples, e.g. (384, 128), (512, 128), (768, 64), run the two-pass kernels.)
+#define TR_BSP_BLK_LIST(X) \
+  X(64, 8, 2, 2) X(64, 6, 2, 2) X(64, 6, 2, 3) X(128, 8, 2, 2) X(128, 6, 2, 2) X(128, 6, 2, 3)
+static bool bsp_blk_compiled(int jt, int nw, int nb) {
+#define TR_BSP_BLK_HAS(J_, NW_, NS_, NB_) \
+  if (jt == J_ && nw == NW_ && nb == NB_) return true;
+  TR_BSP_BLK_LIST(TR_BSP_BLK_HAS)
+#undef TR_BSP_BLK_HAS
+  return false;
+}
 static const void* duo_kernel(const MnlGeom& g, bool exact) {
   if (g.bsp) {
-#define TR_BSP_PTR(J_, NW_, NS_)                                                                          \
-  if (g.du_jt == J_ && g.du_nw == NW_ && g.du_ns == NS_) {                                                 \
+#define TR_BSP_PTR4(J_, NW_, NS_, NB_)                                                                    \
     if (exact)                                                                                            \
-      return g.du_pad ? reinterpret_cast<const void*>(&k_mnl_bsp<J_, NW_, NS_, true, true>)                \
-                      : reinterpret_cast<const void*>(&k_mnl_bsp<J_, NW_, NS_, false, true>);              \
-    return g.du_pad ? reinterpret_cast<const void*>(&k_mnl_bsp<J_, NW_, NS_, true, false>)                 \
-                    : reinterpret_cast<const void*>(&k_mnl_bsp<J_, NW_, NS_, false, false>);               \
-  }
+      return g.du_pad ? reinterpret_cast<const void*>(&k_mnl_bsp<J_, NW_, NS_, true, true, NB_>)          \
+                      : reinterpret_cast<const void*>(&k_mnl_bsp<J_, NW_, NS_, false, true, NB_>);        \
+    return g.du_pad ? reinterpret_cast<const void*>(&k_mnl_bsp<J_, NW_, NS_, true, false, NB_>)           \
+                    : reinterpret_cast<const void*>(&k_mnl_bsp<J_, NW_, NS_, false, false, NB_>);
+#define TR_BSP_PTR(J_, NW_, NS_) \
+  if (g.du_nb == 1 && g.du_jt == J_ && g.du_nw == NW_ && g.du_ns == NS_) { TR_BSP_PTR4(J_, NW_, NS_, 1) }
+#define TR_BSP_BLK_PTR(J_, NW_, NS_, NB_) \
+  if (g.du_nb == NB_ && g.du_jt == J_ && g.du_nw == NW_ && g.du_ns == NS_) { TR_BSP_PTR4(J_, NW_, NS_, NB_) }
     TR_BSP_LIST(TR_BSP_PTR)
+    TR_BSP_BLK_LIST(TR_BSP_BLK_PTR)
 #undef TR_BSP_PTR
+#undef TR_BSP_BLK_PTR
+#undef TR_BSP_PTR4
     return nullptr;
   }
   return g.J == 64 ? reinterpret_cast<const void*>(&k_mnl_duo<64>) : reinterpret_cast<const void*>(&k_mnl_duo<128>);
@@ -1005,6 +1178,8 @@ static int64_t duo_carve(MnlGeom* g, int nw, int64_t spf, int ns) {
   o = (o + 3) & ~(int64_t)3;
   g->bs_oU = (int)o;  // bsp: [ns][NW waves][8 ranks] U partials
   o += ns * nw * 8;
+  g->bs_oTB = (int)o;  // bsp row blocks: [2][nb - 1][NW][NT][128] (T, dPhi0) of the earlier blocks
+  if (g->du_nb > 1) o += 2LL * (g->du_nb - 1) * nw * (g->du_jt == 64 ? 2 : 1) * 128;
   g->du_oG = g->slab <= ns * spf ? 0 : (int)o;  // the arena image aliases the drained ring
   if (g->du_oG) o += g->slab;
   return (o + 3) & ~(int64_t)3;
@@ -1019,6 +1194,7 @@ void mnl_duo_geom(MnlGeom* g) {
   g->du_ns = 2;
   g->du_pad = 0;
   g->du_jt = g->J;
+  g->du_nb = 1;
   const char* env = std::getenv("TR_MNL_DUO");
   if (env != nullptr && env[0] == '0') return;
   // (J from 28 up: padded to 64, J = 32 runs at 46-48 % of HBM against 14-37 % on the fallbacks; at
@@ -1045,24 +1221,45 @@ void mnl_duo_geom(MnlGeom* g) {
   const char* spl = std::getenv("TR_DUO_SPLIT");
   const bool force_split = spl != nullptr && spl[0] == '1', no_split = spl != nullptr && spl[0] == '0';
   const bool rankblock = s32k && g->nrb == 2;
-  const bool bsp = (s32k || wide) && g->R <= 8 && !no_split && (force_split || !rankblock);
-  if (!bsp && !rankblock) return;
-  const int nw = !bsp ? 4 : jt == 64 ? (g->I > 32 ? (g->I + 31) / 32 : 2) : (g->I > 64 ? 2 * ((g->I + 31) / 32) : 4);
+  // taller samples (above 256 rows at J <= 64, 128 at J <= 128) stream through the ring in du_nb row
+  // blocks of 32 NW x 64 / 16 NW x 128, NW = 8 or 6 (one workgroup per CU), the first whose rows
+  // divide I and whose ring plus the earlier blocks' T / dPhi0 images fit the LDS
+  int blk_nw = 0;
+  if (!wide && !s32k && g->R <= 8 && !no_split) {
+    for (const int c : {8, 6}) {
+      const int ib = jt == 64 ? 32 * c : 16 * c;
+      if (g->I % ib != 0 || g->I / ib < 2 || !bsp_blk_compiled(jt, c, g->I / ib)) continue;
+      g->du_nb = g->I / ib;
+      g->du_jt = jt;
+      if (duo_carve(g, c, (int64_t)ib * jt, 2) * 4 <= 160 * 1024) {
+        blk_nw = c;
+        break;
+      }
+      g->du_nb = 1;
+    }
+  }
+  const bool bsp = (s32k || wide || blk_nw) && g->R <= 8 && !no_split && (force_split || !rankblock);
+  if (!bsp && !rankblock) {
+    g->du_nb = 1;
+    return;
+  }
+  const int nw = !bsp ? 4 : blk_nw ? blk_nw : jt == 64 ? (g->I > 32 ? (g->I + 31) / 32 : 2) : (g->I > 64 ? 2 * ((g->I + 31) / 32) : 4);
   g->du_jt = bsp ? jt : g->J;
   const int wpc = 8 / nw;
-  const int64_t spf = (int64_t)(!bsp ? g->I : jt == 64 ? 32 * nw : 16 * nw) * g->du_jt;  // LDS floats per (padded) sample
+  // LDS floats per (padded) sample, or per row block
+  const int64_t spf = (int64_t)(!bsp ? g->I : jt == 64 ? 32 * nw : 16 * nw) * g->du_jt;
   // a padded sample fills at least a third of its padded shape (TR_DUO_ANYFILL=1: any fill, for the
   // tests): below that the two-pass kernels' ~2.6 TB/s on the real bytes beats the body's rate on
   // the padded ones ((16, 64): 25.8 vs 32.3 % of HBM, (24, 48) at 0.28 even, (24, 64) at 0.375 37.5 vs
   // 33.1 %; profiles/r05_mnl_fallbacks.txt)
   const char* anyfill = std::getenv("TR_DUO_ANYFILL");
-  if (bsp && 3 * (int64_t)g->I * g->J < spf && !(anyfill && std::atoi(anyfill) == 1)) return;
+  if (bsp && 3 * (int64_t)g->I * g->J < spf * g->du_nb && !(anyfill && std::atoi(anyfill) == 1)) return;
   auto carve = [&](int ns) { return duo_carve(g, nw, spf, ns); };
   // the split body at NW = 5, 6 (one workgroup per CU: 80 / 96 KiB in flight with two slots) takes
   // a ring of three samples: (160, 64) 58.9 -> 61.4 %, (192, 64) 65.4 -> 68.5 %, (96, 128) 65.8 ->
   // 69.7 % of HBM (tools/mnl_shapes.py, two runs each); at NW = 3 (two workgroups per CU) three
   // slots measured the same as two.
-  const bool ring3_ok = bsp && (nw == 5 || nw == 6) && (jt == 64 || nw == 6);
+  const bool ring3_ok = bsp && g->du_nb == 1 && (nw == 5 || nw == 6) && (jt == 64 || nw == 6);
   int ns = 2;
   if (ring3_ok && wpc * carve(3) * 4 <= 160 * 1024) ns = 3;
   const int64_t o = carve(ns);
@@ -1071,7 +1268,7 @@ void mnl_duo_geom(MnlGeom* g) {
   g->du_nw = nw;
   g->du_wpc = wpc;
   g->du_ns = ns;
-  g->du_pad = bsp && spf != (int64_t)g->I * g->J ? 1 : 0;
+  g->du_pad = bsp && spf * g->du_nb != (int64_t)g->I * g->J ? 1 : 0;
   g->duo = 1;
   g->bsp = bsp ? 1 : 0;
 }
@@ -1116,6 +1313,7 @@ hipError_t mnl_duo_prepare(MnlGeom* g) {
   }
   if (g->bsp && g->full && g->I * g->J == 8192 && g->nrb == 2) {  // the rank-block form instead
     g->bsp = 0;
+    g->du_nb = 1;
     g->du_nw = 4;
     g->du_wpc = 2;
     g->du_ns = 2;
@@ -1128,6 +1326,7 @@ hipError_t mnl_duo_prepare(MnlGeom* g) {
   }
   g->duo = 0;  // k_mnl_fused (where it fits)
   g->bsp = 0;
+  g->du_nb = 1;
   g->du_nw = 4;
   g->du_wpc = 2;
   g->du_ns = 2;
@@ -1143,25 +1342,30 @@ hipError_t launch_mnl_duo(const MnlGeom& g, int grid, const float* X, int64_t N,
   DuArgs a{X, N, xld, phi, w, scale, gpart, dpart, rows_per_wg, reverse};
   const size_t lds = (size_t)g.du_lds_floats * 4;
   if (g.bsp) {
-#define TR_BSP_LAUNCH(J_, NW_, NS_)                                                                       \
-  if (g.du_jt == J_ && g.du_nw == NW_ && g.du_ns == NS_) {                                                 \
+#define TR_BSP_LAUNCH4(J_, NW_, NS_, NB_)                                                                 \
     if (g.du_pad && g.bs_exact)                                                                           \
-      hipLaunchKernelGGL((k_mnl_bsp<J_, NW_, NS_, true, true>), dim3(grid), dim3(NW_ * TR_WAVE), lds, st, g, a, \
-                         lab, class_w, stop);                                                             \
-    else if (g.du_pad)                                                                                    \
-      hipLaunchKernelGGL((k_mnl_bsp<J_, NW_, NS_, true, false>), dim3(grid), dim3(NW_ * TR_WAVE), lds, st, g, a, \
-                         lab, class_w, stop);                                                             \
-    else if (g.bs_exact)                                                                                  \
-      hipLaunchKernelGGL((k_mnl_bsp<J_, NW_, NS_, false, true>), dim3(grid), dim3(NW_ * TR_WAVE), lds, st, g, a, \
-                         lab, class_w, stop);                                                             \
-    else                                                                                                  \
-      hipLaunchKernelGGL((k_mnl_bsp<J_, NW_, NS_, false, false>), dim3(grid), dim3(NW_ * TR_WAVE), lds, st, g, \
+      hipLaunchKernelGGL((k_mnl_bsp<J_, NW_, NS_, true, true, NB_>), dim3(grid), dim3(NW_ * TR_WAVE), lds, st, g, \
                          a, lab, class_w, stop);                                                          \
-    return hipGetLastError();                                                                             \
-  }
+    else if (g.du_pad)                                                                                    \
+      hipLaunchKernelGGL((k_mnl_bsp<J_, NW_, NS_, true, false, NB_>), dim3(grid), dim3(NW_ * TR_WAVE), lds, st,  \
+                         g, a, lab, class_w, stop);                                                       \
+    else if (g.bs_exact)                                                                                  \
+      hipLaunchKernelGGL((k_mnl_bsp<J_, NW_, NS_, false, true, NB_>), dim3(grid), dim3(NW_ * TR_WAVE), lds, st,  \
+                         g, a, lab, class_w, stop);                                                       \
+    else                                                                                                  \
+      hipLaunchKernelGGL((k_mnl_bsp<J_, NW_, NS_, false, false, NB_>), dim3(grid), dim3(NW_ * TR_WAVE), lds, st, \
+                         g, a, lab, class_w, stop);                                                       \
+    return hipGetLastError();
+#define TR_BSP_LAUNCH(J_, NW_, NS_) \
+  if (g.du_nb == 1 && g.du_jt == J_ && g.du_nw == NW_ && g.du_ns == NS_) { TR_BSP_LAUNCH4(J_, NW_, NS_, 1) }
+#define TR_BSP_BLK_LAUNCH(J_, NW_, NS_, NB_) \
+  if (g.du_nb == NB_ && g.du_jt == J_ && g.du_nw == NW_ && g.du_ns == NS_) { TR_BSP_LAUNCH4(J_, NW_, NS_, NB_) }
     TR_BSP_LIST(TR_BSP_LAUNCH)
+    TR_BSP_BLK_LIST(TR_BSP_BLK_LAUNCH)
     return hipErrorInvalidValue;
 #undef TR_BSP_LAUNCH
+#undef TR_BSP_BLK_LAUNCH
+#undef TR_BSP_LAUNCH4
   } else if (g.J == 64) {
     hipLaunchKernelGGL((k_mnl_duo<64>), dim3(grid), dim3(DU_T), lds, st, g, a, lab, class_w, stop);
   } else {

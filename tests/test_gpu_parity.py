@@ -475,6 +475,16 @@ WIDE_SHAPES = [((300, 64, 64), 10, 8), ((200, 96, 64), 7, 3), ((400, 128, 64), 5
                # samples of fewer rows than two 32-row waves (64-wide) or four 16-row waves (128-wide)
                ((300, 16, 64), 10, 8), ((200, 1, 64), 5, 3), ((150, 32, 32), 4, 8), ((400, 8, 128), 6, 5),
                ((90, 32, 128), 3, 2), ((64, 5, 40), 7, 4), ((100, 48, 128), 4, 8), ((50, 3, 28), 3, 1)]
+# (shape, C, rank, waves, row blocks) of samples above the split body's rows, streamed as row blocks
+# of 32 NW x 64 / 16 NW x 128 (NW = 8, else 6): two, three and four blocks, padded widths, fewer
+# samples than workgroups, one rank, one class
+ROWBLOCK_SHAPES = [((150, 512, 64), 10, 8, 8, 2), ((100, 384, 64), 7, 3, 6, 2), ((80, 576, 64), 5, 5, 6, 3),
+                   ((120, 256, 128), 10, 8, 8, 2), ((90, 192, 128), 6, 2, 6, 2), ((70, 288, 128), 3, 7, 6, 3),
+                   ((100, 512, 48), 5, 8, 8, 2), ((70, 256, 100), 3, 4, 8, 2), ((7, 256, 128), 3, 8, 8, 2),
+                   ((50, 512, 64), 2, 1, 8, 2), ((40, 576, 64), 1, 3, 6, 3), ((60, 192, 100), 4, 6, 6, 2)]
+# ... and samples above 64 KiB outside them (rows not a whole number of blocks; no spill-free
+# instantiation of their block count): the two-pass kernels
+ROWBLOCK_OUTSIDE = [((40, 300, 128), 4, 8), ((30, 512, 128), 3, 5), ((30, 768, 64), 5, 4)]
 
 
 def _split_jt(J):
@@ -494,6 +504,8 @@ MNL_SHAPES = [((50, 8, 4), 2, 2), ((200, 16, 8), 10, 4), ((97, 5, 7), 16, 3), ((
               ((1001, 128, 64), 10, 5), ((513, 128, 64), 16, 3), ((2, 128, 64), 2, 8), ((300, 64, 128), 6, 7),
               # its split body on (32 NW, 64) samples, NW = 2..8 (I = 256: k_mnl_fused does not fit)
               *WIDE_SHAPES,
+              # ... and as row blocks (samples above 64 KiB: the two-pass kernels before round 6)
+              *[r[:3] for r in ROWBLOCK_SHAPES], *ROWBLOCK_OUTSIDE,
               # wide classes (C > 16): logits by class tile (MFMA when P % 32 == 0, else VALU),
               # k_softmax_rows, tiled column reduction; rank beyond 64 (MTTKRP rank tiles)
               ((150, 8, 4), 17, 3), ((230, 16, 8), 40, 5), ((99, 5, 7), 33, 2), ((200, 12), 100, 4),
@@ -524,10 +536,27 @@ def test_multinomial_wide_split_body_selected(shape, C, rank, monkeypatch):
         monkeypatch.setenv("TR_DUO_ANYFILL", "1")
     with path("auto"):
         desc = _multinomial_sweep(shape, C, rank)
-    # (the padded (16 NW, 128) body with a ring of three spills at NW = 6: the plan takes two slots)
-    padded = shape[1] != (32 if jt == 64 else 16) * nw or shape[2] != jt
-    nbuf = 3 if nw in (5, 6) and not (padded and jt == 128) else 2
+    # (round 5's padded (16 NW, 128) body with a ring of three spilled at NW = 6 and the plan took two
+    # slots; round 6's epilogue fetches Wv and U by ds_bpermute instead of 12 select registers)
+    nbuf = 3 if nw in (5, 6) else 2
     assert "form=bf16split" in desc and f"waves={nw} wg/cu={8 // nw} nbuf={nbuf} " in desc, desc
+
+
+@pytest.mark.parametrize("shape,C,rank,nw,nb", ROWBLOCK_SHAPES)
+def test_multinomial_row_blocks_selected(shape, C, rank, nw, nb):
+    """Samples taller than the split body's 32 NW x 64 / 16 NW x 128 rows whose rows divide into
+    NW = 8 (else 6) wave blocks take the split body in nb row blocks by default; the results are the
+    sweep's (test_multinomial_sweep_vs_oracle covers every kind on these shapes)."""
+    with path("auto"):
+        desc = _multinomial_sweep(shape, C, rank)
+    assert "form=bf16split" in desc and f"waves={nw} wg/cu=1 nbuf=2 " in desc and f"rowblocks={nb}" in desc, desc
+
+
+@pytest.mark.parametrize("shape,C,rank", ROWBLOCK_OUTSIDE)
+def test_multinomial_row_blocks_outside(shape, C, rank):
+    with path("auto"):
+        desc = _multinomial_sweep(shape, C, rank)
+    assert " duo " not in desc and "path=2pass" in desc, desc
 
 
 def _multinomial_sweep(shape, C, rank):
@@ -569,7 +598,8 @@ SPLIT_SCALE_SHAPES = [((300, 64, 64), 10, 8, "auto"), ((200, 96, 64), 7, 3, "aut
                       ((60, 224, 64), 3, 6, "auto"), ((150, 256, 64), 16, 5, "auto"),
                       ((120, 96, 128), 6, 7, "auto"), ((80, 128, 128), 10, 8, "auto"),
                       ((300, 100, 64), 10, 8, "auto"), ((200, 128, 48), 10, 8, "auto"), ((80, 70, 128), 4, 8, "auto"),
-                      ((256, 128, 64), 10, 3, "auto"), ((256, 128, 64), 10, 8, "split")]
+                      ((256, 128, 64), 10, 3, "auto"), ((256, 128, 64), 10, 8, "split"),
+                      ((64, 256, 128), 10, 8, "auto"), ((40, 512, 64), 7, 5, "auto")]
 
 
 @pytest.mark.parametrize("xscale", [1e-4, 1e-2, 1.0, 1e4, 3e7, "mixed"])

@@ -19,7 +19,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from tensor_regression_amd import _lib  # noqa: E402
 from tensor_regression_amd import CP_logistic_regression  # noqa: E402
 
-N, I, J, C, R = int(os.environ.get("N", 65536)), 128, 64, 10, 8
+# I, J, R from the environment too (the split body's shapes; NW = 8 waves at most, row blocks)
+I, J, R = int(os.environ.get("I", 128)), int(os.environ.get("J", 64)), int(os.environ.get("R", 8))
+N, C = int(os.environ.get("N", 65536 * 8192 // (I * J))), 10
 dev = "cuda:0"
 g = torch.Generator(device=dev).manual_seed(0)
 X = torch.randn(N, I, J, device=dev, generator=g)
@@ -33,12 +35,17 @@ print(m._plan.describe)
 lib = _lib.load()
 fn = lib.tr_duo_profile_read
 fn.restype = ctypes.c_int
-buf = (ctypes.c_ulonglong * (512 * 4 * 4))()
+buf = (ctypes.c_ulonglong * (512 * 8 * 4))()
 assert fn(buf) == 0
-a = np.array(buf[:], dtype=np.float64).reshape(512, 4, 4)
-per_wg = (N + 511) // 512
+a = np.array(buf[:], dtype=np.float64).reshape(512, 8, 4)
+d = m._plan.describe
+nw = int(d.split("waves=")[1].split()[0])
+wpc = int(d.split("wg/cu=")[1].split()[0])
+nb = int(d.split("rowblocks=")[1].split()[0]) if "rowblocks=" in d else 1
+per_wg = (N + 256 * wpc - 1) // (256 * wpc) * nb  # sample blocks per workgroup (one per sample without row blocks)
+a = a[: min(512, 256 * wpc)]
 names = ["DMA wait", "barrier", "GEMM+epi", "tail"]
-print("cycles/sample  " + " ".join(f"{n:>10s}" for n in names) + "      total")
-for w in range(4):
+print(f"cycles/{'block' if nb > 1 else 'sample'}   " + " ".join(f"{n:>10s}" for n in names) + "      total")
+for w in range(nw):
     v = a[:, w, :].mean(axis=0) / per_wg
-    print(f"wave {w} ({'A' if w < 2 else 'B'})    " + " ".join(f"{x:10.0f}" for x in v) + f" {v.sum():10.0f}")
+    print(f"wave {w}          " + " ".join(f"{x:10.0f}" for x in v) + f" {v.sum():10.0f}")

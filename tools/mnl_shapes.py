@@ -21,7 +21,7 @@ from tensor_regression_amd import CP_logistic_regression  # noqa: E402
 dev = "cuda:0"
 SHAPES = [((128, 64), 8), ((64, 128), 8), ((128, 64), 3), ((64, 64), 8), ((96, 64), 8), ((160, 64), 8),
           ((192, 64), 8), ((224, 64), 8), ((256, 64), 8), ((64, 64), 3), ((96, 128), 8), ((128, 128), 8),
-          ((256, 128), 8)]
+          ((256, 128), 8), ((512, 64), 8), ((384, 64), 8), ((768, 64), 8), ((192, 128), 8), ((512, 128), 8)]
 if len(sys.argv) > 1:  # a subset: "I,J" or "I,J,R" arguments (rank 8 by default)
     SHAPES = [((int(a.split(",")[0]), int(a.split(",")[1])), int(a.split(",")[2]) if a.count(",") > 1 else 8)
               for a in sys.argv[1:]]
@@ -47,7 +47,9 @@ for (I, J), R in SHAPES:
     alg = N * (4 * I * J + 8)
     path = plan.describe.split(" path=")[1].split()[0]
     form = (f"duo {plan.describe.split('form=')[1].split()[0]} waves={plan.describe.split('waves=')[1].split()[0]}"
-            f" nbuf={plan.describe.split('nbuf=')[1].split()[0]}" if " duo " in plan.describe else path)
+            f" nbuf={plan.describe.split('nbuf=')[1].split()[0]}"
+            + (f" blocks={plan.describe.split('rowblocks=')[1].split()[0]}" if "rowblocks=" in plan.describe else "")
+            if " duo " in plan.describe else path)
     print(f"(N, I, J) = ({N}, {I}, {J}) R={R}: {form:32s} stream kernels {tot:.4f} ms = "
           f"{alg / (tot * 1e-3) / 1e12:.2f} TB/s = {alg / (tot * 1e-3) / 8e12 * 100:.1f} % of HBM  {ms}", flush=True)
     del m, X, y
