@@ -43,7 +43,8 @@ struct MnlGeom {
   int du_oZ, du_oP1, du_oG, du_lds_floats;
   // bf16-split form of the duo family (k_mnl_bsp: a 32 KiB (128, 64) or (64, 128) sample at
   // rank <= 4, and every (32 NW, 64) sample with NW = 2..8 and (16 NW, 128) sample with NW = 4, 6,
-  // 8 at rank <= 8 (other I, and J % 4 == 0 of 28..128, padded to the next), C <= 16; TR_DUO_SPLIT=1
+  // 8 at rank <= 8 (other I, and J % 4 == 0 of 28..128, padded to the next; taller samples as du_nb
+  // row blocks of those), C <= 16; TR_DUO_SPLIT=1
   // takes it at (128, 64) / (64, 128) rank 5..8 too, =0 keeps the rank-block form): U partials at bs_oU
   int bsp, bs_oU;
   // split body's X form (tr_plan_set_x_range): 0 = bf16 + f16 residual, 1 = three exact bf16 pieces
