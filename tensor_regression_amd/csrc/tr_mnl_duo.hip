@@ -566,7 +566,7 @@ __device__ __forceinline__ void for_each_ic(std::integer_sequence<int, T...>, F&
   (f(std::integral_constant<int, T>()), ...);
 }
 
-template <int JT, int NW, int NS, bool PAD, bool EXACT, int NB>
+template <int JT, int NW, int NS, bool PAD, bool EXACT, int NB, int RK>
 __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, const int64_t* __restrict__ lab,
                                          const float* __restrict__ class_w, float* lds, const int wv, const int lane) {
   const int t = threadIdx.x;
@@ -588,17 +588,27 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
   constexpr bool BLK = NB > 1;
   constexpr int nb = NB;
   static_assert(!BLK || NS == 2, "row blocks: a ring of two");
+  // RK = 16 (ranks 9..16): the accumulator's 16 columns are 16 ranks of one piece (B operands b1,
+  // b2, b3 and the f16 h in four registers each, one MFMA per piece: 4 per tile and k step in the
+  // fast form, 6 in the exact one) instead of 8 ranks x two pieces folded (RK = 8: 3 / 4); the
+  // epilogue's DPP row gq carries ranks gq + 4 k, k < RK / 4
+  static_assert(RK == 8 || RK == 16, "8 or 16 rank columns");
+  constexpr bool R16 = RK == 16;
+  constexpr int KR = RK / 4;  // ranks per epilogue row
+  static_assert(!(BLK && R16), "row blocks at rank <= 8");
   const int Ir = (PAD && !BLK) ? g.I : I, Jr = PAD ? g.J : J;
   // NS = 3: a ring of three samples (the DMA of sample k + 2 goes into the slot of k - 1 while k
   // is computed: two samples in flight), where three fit the workgroup's LDS share
   static_assert(NS == 2 || NS == 3, "ring of two or three slots");
-  float* sU = lds + g.bs_oU;  // [NS slots][NW waves][8 ranks] U partials
+  float* sU = lds + g.bs_oU;  // [NS slots][NW waves][RK ranks] U partials
   const float* P0 = a.phi;
   const float* P1 = a.phi + g.offP1;
   const float* PC = a.phi + g.offPC;
-  const int n = lane & 15, gq = lane >> 4, r8 = n & 7;
-  const bool lo8 = n < 8, rok = r8 < R;
-  const int c = n;  // epilogue: class lane c, DPP row gq (ranks gq and gq + 4)
+  // r8: the rank of this lane's accumulator column (RK = 8: columns r and r + 8 hold two pieces of
+  // rank r, lanes n >= 8 duplicate it after the fold and weigh 0; RK = 16: rank n)
+  const int n = lane & 15, gq = lane >> 4, r8 = R16 ? n : n & 7;
+  const bool lo8 = R16 || n < 8, rok = r8 < R;
+  const int c = n;  // epilogue: class lane c, DPP row gq (ranks gq + 4 k)
   const bool cok = c < C;
   const float cwl = cok ? class_w[c] : 0.f;
   const float NEG = -__builtin_huge_valf();
@@ -607,19 +617,29 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
   const int iv0 = JT == 64 ? 32 * wv : 32 * (wv % NKS);           // V k-step (rows) of this wave
   const int cv = n + (J == 128 ? 16 * (wv / NKS) : 0);            // V chunk (j = 4 cv + tile)
   // B operands, split once per launch: T (Phi1, element e of lane group gq <-> j = 32 s + 8 gq + e)
-  uint32_t bT12[NKT][4], bT3[NKT][4], hT[NKT][4], bV12[4], bV3[4], hV[4];
-  auto bsplit = [&](float x0, float x1, uint32_t& b12, uint32_t& b3, uint32_t& hh) {
+  // (RK = 16: bT12 / bV12 hold b1, bT2 / bV2 b2, bT3 / bV3 b3, hT / hV f16(x))
+  constexpr int N2 = R16 ? NKT : 1;
+  uint32_t bT12[NKT][4], bT2[N2][4], bT3[NKT][4], hT[NKT][4], bV12[4], bV2[4], bV3[4], hV[4];
+  auto bsplit = [&](float x0, float x1, uint32_t& b12, uint32_t& b2, uint32_t& b3, uint32_t& hh) {
     uint32_t h1, h2, h3;
     sl_split2(x0, x1, h1, h2, h3);
-    b12 = lo8 ? h1 : h2;
-    b3 = lo8 ? h3 : 0u;
-    if constexpr (!EXACT) {  // f16 pieces for the fast form's f16 X piece: [f16(x) | f16(x - f16(x))]
-      const uint32_t f1 = bs_pack_h(x0, x1);
-      const bs_h2 f1v = __builtin_bit_cast(bs_h2, f1);
-      const uint32_t f2 = bs_pack_h(x0 - (float)f1v[0], x1 - (float)f1v[1]);
-      hh = lo8 ? f1 : f2;
+    if constexpr (R16) {
+      b12 = h1;
+      b2 = h2;
+      b3 = h3;
+      hh = EXACT ? 0u : bs_pack_h(x0, x1);
     } else {
-      hh = 0u;
+      b12 = lo8 ? h1 : h2;
+      b2 = 0u;
+      b3 = lo8 ? h3 : 0u;
+      if constexpr (!EXACT) {  // f16 pieces for the fast form's f16 X piece: [f16(x) | f16(x - f16(x))]
+        const uint32_t f1 = bs_pack_h(x0, x1);
+        const bs_h2 f1v = __builtin_bit_cast(bs_h2, f1);
+        const uint32_t f2 = bs_pack_h(x0 - (float)f1v[0], x1 - (float)f1v[1]);
+        hh = lo8 ? f1 : f2;
+      } else {
+        hh = 0u;
+      }
     }
   };
 #pragma unroll
@@ -628,7 +648,8 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
     for (int v = 0; v < 4; ++v) {
       const int j = 32 * s + 8 * gq + 2 * v;
       bsplit((rok && (!PAD || j < Jr)) ? P1[(int64_t)j * R + r8] : 0.f,
-             (rok && (!PAD || j + 1 < Jr)) ? P1[(int64_t)(j + 1) * R + r8] : 0.f, bT12[s][v], bT3[s][v], hT[s][v]);
+             (rok && (!PAD || j + 1 < Jr)) ? P1[(int64_t)(j + 1) * R + r8] : 0.f, bT12[s][v], bT2[R16 ? s : 0][v],
+             bT3[s][v], hT[s][v]);
     }
   // V (Phi0, element e <-> i = iv0 + 8 gq + e) and the U weights: T accumulator (lane (n, gq), reg
   // v) = T[it0 + 16 tt + 4 gq + v][n & 7] after the column fold; lanes n >= 8 hold the same values
@@ -669,7 +690,7 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
   };
   auto split_rows = [&]() {
 #pragma unroll
-    for (int v = 0; v < 4; ++v) bsplit(pvr[2 * v], pvr[2 * v + 1], bV12[v], bV3[v], hV[v]);
+    for (int v = 0; v < 4; ++v) bsplit(pvr[2 * v], pvr[2 * v + 1], bV12[v], bV2[v], bV3[v], hV[v]);
     if constexpr (BLK)  // the U weights' loads complete here too, before this block's first LDS-DMA piece
 #pragma unroll
       for (int tt = 0; tt < NT; ++tt)
@@ -678,19 +699,29 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
   };
   load_rows(0, phiU);
   if constexpr (!BLK) split_rows();
-  // epilogue weights: pc[r] = w_r PhiC[c][r]; row gq's ranks gq, gq + 4.  BLK reads pc[r] from an
-  // LDS table [class 16][rank 8] (the rank-block body's Z slots, unused here) in the epilogue: the
-  // row-block form needs the 8 registers
+  // epilogue weights: pc[r] = w_r PhiC[c][r]; row gq's ranks gq + 4 k.  BLK and RK = 16 read them
+  // from an LDS table in the rank-block body's Phi1 slots (unused here) in the epilogue: those forms
+  // need the registers
+  constexpr bool PCL = BLK || R16;  // pc[] from the LDS table
   float pc[8];
 #pragma unroll
-  for (int r = 0; r < 8; ++r) pc[r] = (!BLK && cok && r < R) ? a.w[r] * PC[c * R + r] : 0.f;
-  auto pc_of = [&](int r) { return (cok && r < R) ? a.w[r] * PC[c * R + r] : 0.f; };
-  const float pcg0 = BLK ? pc_of(gq) : pc[gq & 3], pcg1 = BLK ? pc_of(gq + 4) : pc[4 + (gq & 3)];
-  float* sPC = lds + g.du_oZ;
-  if constexpr (BLK)
-    for (int e = t; e < 128; e += NT_) sPC[e] = (e / 8 < C && e % 8 < R) ? a.w[e % 8] * PC[(e / 8) * R + e % 8] : 0.f;
-  const float wg0 = gq < R ? a.w[gq] : 0.f, wg1 = gq + 4 < R ? a.w[gq + 4] : 0.f;
-  for (int e = t; e < NS * NW * 8; e += NT_) sU[e] = 0.f;
+  for (int r = 0; r < 8; ++r) pc[r] = (!PCL && cok && r < R) ? a.w[r] * PC[c * R + r] : 0.f;
+  // row gq's ranks gq + 4 k: pc and w (PCL: read from the table in the epilogue stage that uses them)
+  float pcg[PCL ? 1 : KR], wg[PCL ? 1 : KR];
+#pragma unroll
+  for (int k = 0; k < (PCL ? 1 : KR); ++k) {
+    pcg[k] = pc[4 * k + (gq & 3)];
+    wg[k] = gq + 4 * k < R ? a.w[gq + 4 * k] : 0.f;
+  }
+  // PCL table: [class 16][RK] pc, then [RK] w
+  float* sPC = lds + g.du_oP1;
+  if constexpr (PCL)
+    for (int e = t; e < 16 * RK + RK; e += NT_)
+      sPC[e] = e >= 16 * RK ? (e - 16 * RK < R ? a.w[e - 16 * RK] : 0.f)
+                            : (e / RK < C && e % RK < R) ? a.w[e % RK] * PC[(e / RK) * R + e % RK] : 0.f;
+  auto pcg_of = [&](int k) { return PCL ? sPC[RK * c + gq + 4 * k] : pcg[k]; };
+  auto wg_of = [&](int k) { return PCL ? sPC[16 * RK + gq + 4 * k] : wg[k]; };
+  for (int e = t; e < NS * NW * RK; e += NT_) sU[e] = 0.f;
   // BLK: the folded T of blocks 0 .. nb - 2 of the previous sample and this wave's dPhi0 rows of
   // those blocks, [2][nb - 1][NW][NT][gq][rank 8][v 4] (lanes n < 8 only; the last block's in registers)
   float* sTB = lds + g.bs_oTB;
@@ -740,7 +771,9 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
   for (int q = 0; q < NT; ++q) gT[q] = du_f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int q = 0; q < 4; ++q) gV[q] = du_f32x4{0.f, 0.f, 0.f, 0.f};
-  float dpc0 = 0.f, dpc1 = 0.f;  // wave 0: dPhiC[c][gq], dPhiC[c][gq + 4]
+  float dpc[KR];  // wave 0: dPhiC[c][gq + 4 k]
+#pragma unroll
+  for (int k = 0; k < KR; ++k) dpc[k] = 0.f;
   double lsum = 0.0;
   du_f32x4 TP[NT], VP[4];  // the previous sample's T and V (folded), for its epilogue
 #pragma unroll
@@ -755,28 +788,29 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
   // (the stages' values, one instance per epilogue: an instance shared across iterations would be
   // carried around the BLK loop, whose stages run only in a sample's first block)
   struct EpiSt {
-    float uS, uR[8];
+    float uS, uR[RK];
     float e_x, e_ez, e_sum, e_S, e_q, e_Sq, e_Sy;
-    float e_s2, e_d1, e_e1, e_dz, e_a0, e_b0, e_y0, e_a1, e_b1, e_y1, e_w0, e_w1, e_wv;
+    float e_s2, e_d1, e_e1, e_dz, e_a[KR], e_b[KR], e_y[KR], e_w[KR], e_wv;
     bool e_isy;
   };
   auto epi = [&](EpiSt& E, int st, int zs, int64_t yE, float cwE) {
     if (TR_DUO_SKIP & 4) return;
     if (st == 0) {  // U[r] = sum of the NW waves' partials (lane r), wave order
-      const float* pu = sU + zs * (8 * NW) + r8;
+      const float* pu = sU + zs * (RK * NW) + r8;
       E.uS = pu[0];
 #pragma unroll
-      for (int w = 1; w < NW; ++w) E.uS += pu[8 * w];
+      for (int w = 1; w < NW; ++w) E.uS += pu[RK * w];
     } else if (st == 1) {
 #pragma unroll
-      for (int r = 0; r < 8; ++r) E.uR[r] = du_rdl(E.uS, r);
+      for (int r = 0; r < RK; ++r) E.uR[r] = du_rdl(E.uS, r);
       float zz;
-      if constexpr (BLK) {
-        const du_f32x4 p0 = *reinterpret_cast<const du_f32x4*>(sPC + 8 * c);
-        const du_f32x4 p1 = *reinterpret_cast<const du_f32x4*>(sPC + 8 * c + 4);
-        zz = p0[0] * E.uR[0];
+      if constexpr (PCL) {
+        du_f32x4 pq[RK / 4];
 #pragma unroll
-        for (int r = 1; r < 8; ++r) zz = fmaf(r < 4 ? p0[r] : p1[r - 4], E.uR[r], zz);
+        for (int h = 0; h < RK / 4; ++h) pq[h] = *reinterpret_cast<const du_f32x4*>(sPC + RK * c + 4 * h);
+        zz = pq[0][0] * E.uR[0];
+#pragma unroll
+        for (int r = 1; r < RK; ++r) zz = fmaf(pq[r / 4][r % 4], E.uR[r], zz);
       } else {
         zz = pc[0] * E.uR[0];
 #pragma unroll
@@ -797,12 +831,13 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
       E.e_s2 = du_row_sum16(E.e_q);
       E.e_d1 = du_row_sum16(E.e_Sq);
       E.e_e1 = du_row_sum16(E.e_Sy);
-      E.e_a0 = du_row_sum16(E.e_Sq * pcg0);
-      E.e_b0 = du_row_sum16(E.e_S * pcg0);
-      E.e_y0 = du_row_sum16(E.e_Sy * pcg0);
-      E.e_a1 = du_row_sum16(E.e_Sq * pcg1);
-      E.e_b1 = du_row_sum16(E.e_S * pcg1);
-      E.e_y1 = du_row_sum16(E.e_Sy * pcg1);
+#pragma unroll
+      for (int k = 0; k < KR; ++k) {
+        const float pk = pcg_of(k);
+        E.e_a[k] = du_row_sum16(E.e_Sq * pk);
+        E.e_b[k] = du_row_sum16(E.e_S * pk);
+        E.e_y[k] = du_row_sum16(E.e_Sy * pk);
+      }
     } else if (st == 5) {
       const float is2 = __builtin_amdgcn_rcpf(E.e_s2);
       const float kk = cwE * a.scale;
@@ -810,15 +845,18 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
       lsum += (wv == 0 && lane == 0) ? (double)cwE * (double)(du_log(E.e_s2) - E.e_e1) : 0.0;
       const float dS = cok ? kk * (E.e_q * is2 - (E.e_isy ? 1.0f : 0.0f)) : 0.f;
       E.e_dz = cok ? E.e_S * (dS - dot) : 0.f;
-      E.e_w0 = kk * (E.e_a0 * is2 - E.e_y0) - dot * E.e_b0;  // Wv[gq]
-      E.e_w1 = kk * (E.e_a1 * is2 - E.e_y1) - dot * E.e_b1;  // Wv[gq + 4]
+#pragma unroll
+      for (int k = 0; k < KR; ++k) E.e_w[k] = kk * (E.e_a[k] * is2 - E.e_y[k]) - dot * E.e_b[k];  // Wv[gq + 4 k]
     } else if (st == 6) {
-      // Wv[r] of this lane's accumulator rank r = n & 7 (rank r < 4: row r's e_w0, else row r - 4's
-      // e_w1), fetched from lane 16 (r & 3)
+      // Wv[r] of this lane's accumulator rank r: row (r & 3)'s e_w[r >> 2], fetched from lane 16 (r & 3)
       const int src = 64 * (r8 & 3);
-      const float w0 = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(E.e_w0)));
-      const float w1 = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(E.e_w1)));
-      E.e_wv = r8 < 4 ? w0 : w1;
+      float wk[KR];
+#pragma unroll
+      for (int k = 0; k < KR; ++k) wk[k] = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(E.e_w[k])));
+      if constexpr (R16)
+        E.e_wv = r8 < 8 ? (r8 < 4 ? wk[0] : wk[1]) : (r8 < 12 ? wk[2] : wk[3]);
+      else
+        E.e_wv = r8 < 4 ? wk[0] : wk[1];
     } else {
 #pragma unroll
       for (int q = 0; q < NT; ++q) gT[q] += E.e_wv * TP[q];
@@ -835,11 +873,12 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
               *gp += E.e_wv * tp;
             }
       }
-      if (wv == 0) {  // dPhiC[c][r] += dZ[c] w_r U[r], r = gq, gq + 4
-        const float u0 = __int_as_float(__builtin_amdgcn_ds_bpermute(4 * gq, __float_as_int(E.uS)));  // U[gq]
-        const float u1 = __int_as_float(__builtin_amdgcn_ds_bpermute(4 * gq + 16, __float_as_int(E.uS)));  // U[gq + 4]
-        dpc0 = fmaf(E.e_dz, wg0 * u0, dpc0);
-        dpc1 = fmaf(E.e_dz, wg1 * u1, dpc1);
+      if (wv == 0) {  // dPhiC[c][r] += dZ[c] w_r U[r], r = gq + 4 k
+#pragma unroll
+        for (int k = 0; k < KR; ++k) {
+          const float uk = __int_as_float(__builtin_amdgcn_ds_bpermute(4 * gq + 16 * k, __float_as_int(E.uS)));  // U[gq + 4 k]
+          dpc[k] = fmaf(E.e_dz, wg_of(k) * uk, dpc[k]);
+        }
       }
     }
   };
@@ -954,15 +993,31 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
         }
       };
       // smallest products first into the accumulator
-      auto gemm = [&](du_f32x4& acc, const uint32_t (&b12)[4], const uint32_t (&b3)[4], const uint32_t (&hh)[4]) {
-        if constexpr (EXACT) {
-          acc = bs_mfma(x3, b12, acc);
-          acc = bs_mfma(x2, b12, acc);
+      // (RK = 16: acc += x3 b1 + x2 b2 + x2 b1 + x1 b3 + x1 b2 + x1 b1 exact, x2 h + x1 b3 + x1 b2 +
+      // x1 b1 fast; dropped x3 b2, x2 b3, x3 b3: < 2^-25 |x b|)
+      auto gemm = [&](du_f32x4& acc, const uint32_t (&b12)[4], const uint32_t (&b2)[4], const uint32_t (&b3)[4],
+                      const uint32_t (&hh)[4]) {
+        if constexpr (R16) {
+          if constexpr (EXACT) {
+            acc = bs_mfma(x3, b12, acc);
+            acc = bs_mfma(x2, b2, acc);
+            acc = bs_mfma(x2, b12, acc);
+          } else {
+            acc = bs_mfma_h(x2, hh, acc);
+          }
+          acc = bs_mfma(x1, b3, acc);
+          acc = bs_mfma(x1, b2, acc);
+          acc = bs_mfma(x1, b12, acc);
         } else {
-          acc = bs_mfma_h(x2, hh, acc);
+          if constexpr (EXACT) {
+            acc = bs_mfma(x3, b12, acc);
+            acc = bs_mfma(x2, b12, acc);
+          } else {
+            acc = bs_mfma_h(x2, hh, acc);
+          }
+          acc = bs_mfma(x1, b3, acc);
+          acc = bs_mfma(x1, b12, acc);
         }
-        acc = bs_mfma(x1, b3, acc);
-        acc = bs_mfma(x1, b12, acc);
       };
       if (st < NU) {
 #pragma unroll
@@ -971,12 +1026,12 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
           split(xr[2 * (v & 1)], xr[2 * (v & 1) + 1], v);
         }
         const int tt = st / NKT, s = st - tt * NKT;
-        gemm(aT[tt], bT12[s], bT3[s], hT[s]);
+        gemm(aT[tt], bT12[s], bT2[R16 ? s : 0], bT3[s], hT[s]);
       } else {
         const int tv = st - NU;  // j-tile: element tv of each row's chunk
 #pragma unroll
         for (int v = 0; v < 4; ++v) split(xv[2 * v][tv], xv[2 * v + 1][tv], v);
-        gemm(aV[tv], bV12, bV3, hV);
+        gemm(aV[tv], bV12, bV2, bV3, hV);
       }
       if (bfirst && st >= 1 && st <= 7) epi(E, st, zsP, yP, cwP);  // (bfirst, st: compile-time)
       __builtin_amdgcn_sched_barrier(0);
@@ -988,7 +1043,7 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
     for (int tt = 0; tt < NT; ++tt) {
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
-        aT[tt][v] += du_dpp<0x128>(aT[tt][v]);  // row_ror:8
+        if constexpr (!R16) aT[tt][v] += du_dpp<0x128>(aT[tt][v]);  // row_ror:8
         u = fmaf(phiU[tt][v], aT[tt][v], u);
       }
       if (blast) {
@@ -1014,11 +1069,12 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
 #pragma unroll
-        for (int v = 0; v < 4; ++v) aV[q][v] += du_dpp<0x128>(aV[q][v]);
+        for (int v = 0; v < 4; ++v)
+          if constexpr (!R16) aV[q][v] += du_dpp<0x128>(aV[q][v]);
         VP[q] = aV[q];
       }
-      u = du_xor32_sum(du_xor16_sum(u));  // lane (n < 8, any row): this wave's U partial of rank n
-      if (lane < 8) sU[zsC * (8 * NW) + wv * 8 + lane] = u;
+      u = du_xor32_sum(du_xor16_sum(u));  // lane (n < RK, any row): this wave's U partial of rank n
+      if (lane < RK) sU[zsC * (RK * NW) + wv * RK + lane] = u;
       yP = yC;
       cwP = cwC;
     }
@@ -1087,8 +1143,9 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
         }
     }
     if (ws == wv && wv == 0 && cok) {
-      if (gq < R) sG[g.offPC + c * R + gq] += dpc0;
-      if (gq + 4 < R) sG[g.offPC + c * R + gq + 4] += dpc1;
+#pragma unroll
+      for (int k = 0; k < KR; ++k)
+        if (gq + 4 * k < R) sG[g.offPC + c * R + gq + 4 * k] += dpc[k];
     }
     __syncthreads();
   }
@@ -1105,7 +1162,7 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
 
 // NW waves per workgroup, 8 / NW workgroups per CU (the second bound is waves per SIMD: two,
 // 256 VGPRs each), a ring of NS samples
-template <int JT, int NW, int NS, bool PAD, bool EXACT, int NB>
+template <int JT, int NW, int NS, bool PAD, bool EXACT, int NB, int RK>
 __global__ __launch_bounds__(NW * TR_WAVE, 2) void k_mnl_bsp(MnlGeom g, DuArgs a, const int64_t* __restrict__ lab,
                                                                const float* __restrict__ class_w,
                                                                const int32_t* __restrict__ stop) {
@@ -1113,7 +1170,7 @@ __global__ __launch_bounds__(NW * TR_WAVE, 2) void k_mnl_bsp(MnlGeom g, DuArgs a
   if (stop != nullptr && *stop != 0) return;
   const int lane = threadIdx.x & (TR_WAVE - 1);
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / TR_WAVE);
-  bsp_body<JT, NW, NS, PAD, EXACT, NB>(g, a, lab, class_w, lds, wv, lane);
+  bsp_body<JT, NW, NS, PAD, EXACT, NB, RK>(g, a, lab, class_w, lds, wv, lane);
 }
 
 template <int JT>
@@ -1139,6 +1196,11 @@ __global__ __launch_bounds__(DU_T, 2) void k_mnl_duo(MnlGeom g, DuArgs a, const 
 // four-block form spill: such samples, e.g. (384, 128), (512, 128), (768, 64), run the two-pass kernels.)
 #define TR_BSP_BLK_LIST(X) \
   X(64, 8, 2, 2) X(64, 6, 2, 2) X(64, 6, 2, 3) X(128, 8, 2, 2) X(128, 6, 2, 2) X(128, 6, 2, 3)
+// ... and its 16-rank instantiations (ranks 9..16; J, NW, ring slots).  (128, 6) with a ring of three
+// spills; so does the padded (128, 8) form, whose samples run k_mnl_fused or the two-pass kernels.
+#define TR_BSP_R16_LIST(X) \
+  X(64, 2, 2) X(64, 3, 2) X(64, 4, 2) X(64, 5, 2) X(64, 5, 3) X(64, 6, 2) X(64, 6, 3) X(64, 7, 2) \
+  X(64, 8, 2) X(128, 4, 2) X(128, 6, 2) X(128, 8, 2)
 static bool bsp_blk_compiled(int jt, int nw, int nb) {
 #define TR_BSP_BLK_HAS(J_, NW_, NS_, NB_) \
   if (jt == J_ && nw == NW_ && nb == NB_) return true;
@@ -1148,21 +1210,31 @@ static bool bsp_blk_compiled(int jt, int nw, int nb) {
 }
 static const void* duo_kernel(const MnlGeom& g, bool exact) {
   if (g.bsp) {
-#define TR_BSP_PTR4(J_, NW_, NS_, NB_)                                                                    \
+#define TR_BSP_PTR5(J_, NW_, NS_, NB_, RK_)                                                               \
     if (exact)                                                                                            \
-      return g.du_pad ? reinterpret_cast<const void*>(&k_mnl_bsp<J_, NW_, NS_, true, true, NB_>)          \
-                      : reinterpret_cast<const void*>(&k_mnl_bsp<J_, NW_, NS_, false, true, NB_>);        \
-    return g.du_pad ? reinterpret_cast<const void*>(&k_mnl_bsp<J_, NW_, NS_, true, false, NB_>)           \
-                    : reinterpret_cast<const void*>(&k_mnl_bsp<J_, NW_, NS_, false, false, NB_>);
-#define TR_BSP_PTR(J_, NW_, NS_) \
-  if (g.du_nb == 1 && g.du_jt == J_ && g.du_nw == NW_ && g.du_ns == NS_) { TR_BSP_PTR4(J_, NW_, NS_, 1) }
-#define TR_BSP_BLK_PTR(J_, NW_, NS_, NB_) \
-  if (g.du_nb == NB_ && g.du_jt == J_ && g.du_nw == NW_ && g.du_ns == NS_) { TR_BSP_PTR4(J_, NW_, NS_, NB_) }
+      return g.du_pad ? reinterpret_cast<const void*>(&k_mnl_bsp<J_, NW_, NS_, true, true, NB_, RK_>)      \
+                      : reinterpret_cast<const void*>(&k_mnl_bsp<J_, NW_, NS_, false, true, NB_, RK_>);    \
+    return g.du_pad ? reinterpret_cast<const void*>(&k_mnl_bsp<J_, NW_, NS_, true, false, NB_, RK_>)       \
+                    : reinterpret_cast<const void*>(&k_mnl_bsp<J_, NW_, NS_, false, false, NB_, RK_>);
+#define TR_BSP_PTR(J_, NW_, NS_)                                                                          \
+  if (g.bs_rk == 8 && g.du_nb == 1 && g.du_jt == J_ && g.du_nw == NW_ && g.du_ns == NS_) {                 \
+    TR_BSP_PTR5(J_, NW_, NS_, 1, 8)                                                                       \
+  }
+#define TR_BSP_BLK_PTR(J_, NW_, NS_, NB_)                                                                 \
+  if (g.bs_rk == 8 && g.du_nb == NB_ && g.du_jt == J_ && g.du_nw == NW_ && g.du_ns == NS_) {               \
+    TR_BSP_PTR5(J_, NW_, NS_, NB_, 8)                                                                     \
+  }
+#define TR_BSP_R16_PTR(J_, NW_, NS_)                                                                      \
+  if (g.bs_rk == 16 && g.du_nb == 1 && g.du_jt == J_ && g.du_nw == NW_ && g.du_ns == NS_) {                \
+    TR_BSP_PTR5(J_, NW_, NS_, 1, 16)                                                                      \
+  }
     TR_BSP_LIST(TR_BSP_PTR)
     TR_BSP_BLK_LIST(TR_BSP_BLK_PTR)
+    TR_BSP_R16_LIST(TR_BSP_R16_PTR)
 #undef TR_BSP_PTR
 #undef TR_BSP_BLK_PTR
-#undef TR_BSP_PTR4
+#undef TR_BSP_R16_PTR
+#undef TR_BSP_PTR5
     return nullptr;
   }
   return g.J == 64 ? reinterpret_cast<const void*>(&k_mnl_duo<64>) : reinterpret_cast<const void*>(&k_mnl_duo<128>);
@@ -1177,8 +1249,8 @@ static int64_t duo_carve(MnlGeom* g, int nw, int64_t spf, int ns) {
   g->du_oP1 = (int)o;
   o += 8LL * (g->du_jt + 4);
   o = (o + 3) & ~(int64_t)3;
-  g->bs_oU = (int)o;  // bsp: [ns][NW waves][8 ranks] U partials
-  o += ns * nw * 8;
+  g->bs_oU = (int)o;  // bsp: [ns][NW waves][bs_rk ranks] U partials
+  o += ns * nw * (g->bs_rk == 16 ? 16 : 8);
   g->bs_oTB = (int)o;  // bsp row blocks: [2][nb - 1][NW][NT][128] (T, dPhi0) of the earlier blocks
   if (g->du_nb > 1) o += 2LL * (g->du_nb - 1) * nw * (g->du_jt == 64 ? 2 : 1) * 128;
   g->du_oG = g->slab <= ns * spf ? 0 : (int)o;  // the arena image aliases the drained ring
@@ -1196,6 +1268,7 @@ void mnl_duo_geom(MnlGeom* g) {
   g->du_pad = 0;
   g->du_jt = g->J;
   g->du_nb = 1;
+  g->bs_rk = g->R > 8 ? 16 : 8;  // the split body's rank columns
   const char* env = std::getenv("TR_MNL_DUO");
   if (env != nullptr && env[0] == '0') return;
   // (J from 28 up: padded to 64, J = 32 runs at 46-48 % of HBM against 14-37 % on the fallbacks; at
@@ -1239,7 +1312,7 @@ void mnl_duo_geom(MnlGeom* g) {
       g->du_nb = 1;
     }
   }
-  const bool bsp = (s32k || wide || blk_nw) && g->R <= 8 && !no_split && (force_split || !rankblock);
+  const bool bsp = (s32k || wide || blk_nw) && g->R <= 16 && !no_split && (force_split || !rankblock);
   if (!bsp && !rankblock) {
     g->du_nb = 1;
     return;
@@ -1260,7 +1333,7 @@ void mnl_duo_geom(MnlGeom* g) {
   // a ring of three samples: (160, 64) 58.9 -> 61.4 %, (192, 64) 65.4 -> 68.5 %, (96, 128) 65.8 ->
   // 69.7 % of HBM (tools/mnl_shapes.py, two runs each); at NW = 3 (two workgroups per CU) three
   // slots measured the same as two.
-  const bool ring3_ok = bsp && g->du_nb == 1 && (nw == 5 || nw == 6) && (jt == 64 || nw == 6);
+  const bool ring3_ok = bsp && g->du_nb == 1 && (nw == 5 || nw == 6) && (jt == 64 || (nw == 6 && g->bs_rk == 8));
   int ns = 2;
   if (ring3_ok && wpc * carve(3) * 4 <= 160 * 1024) ns = 3;
   const int64_t o = carve(ns);
@@ -1343,30 +1416,40 @@ hipError_t launch_mnl_duo(const MnlGeom& g, int grid, const float* X, int64_t N,
   DuArgs a{X, N, xld, phi, w, scale, gpart, dpart, rows_per_wg, reverse};
   const size_t lds = (size_t)g.du_lds_floats * 4;
   if (g.bsp) {
-#define TR_BSP_LAUNCH4(J_, NW_, NS_, NB_)                                                                 \
+#define TR_BSP_LAUNCH5(J_, NW_, NS_, NB_, RK_)                                                            \
     if (g.du_pad && g.bs_exact)                                                                           \
-      hipLaunchKernelGGL((k_mnl_bsp<J_, NW_, NS_, true, true, NB_>), dim3(grid), dim3(NW_ * TR_WAVE), lds, st, g, \
-                         a, lab, class_w, stop);                                                          \
+      hipLaunchKernelGGL((k_mnl_bsp<J_, NW_, NS_, true, true, NB_, RK_>), dim3(grid), dim3(NW_ * TR_WAVE), lds, \
+                         st, g, a, lab, class_w, stop);                                                   \
     else if (g.du_pad)                                                                                    \
-      hipLaunchKernelGGL((k_mnl_bsp<J_, NW_, NS_, true, false, NB_>), dim3(grid), dim3(NW_ * TR_WAVE), lds, st,  \
-                         g, a, lab, class_w, stop);                                                       \
+      hipLaunchKernelGGL((k_mnl_bsp<J_, NW_, NS_, true, false, NB_, RK_>), dim3(grid), dim3(NW_ * TR_WAVE), lds, \
+                         st, g, a, lab, class_w, stop);                                                   \
     else if (g.bs_exact)                                                                                  \
-      hipLaunchKernelGGL((k_mnl_bsp<J_, NW_, NS_, false, true, NB_>), dim3(grid), dim3(NW_ * TR_WAVE), lds, st,  \
-                         g, a, lab, class_w, stop);                                                       \
+      hipLaunchKernelGGL((k_mnl_bsp<J_, NW_, NS_, false, true, NB_, RK_>), dim3(grid), dim3(NW_ * TR_WAVE), lds, \
+                         st, g, a, lab, class_w, stop);                                                   \
     else                                                                                                  \
-      hipLaunchKernelGGL((k_mnl_bsp<J_, NW_, NS_, false, false, NB_>), dim3(grid), dim3(NW_ * TR_WAVE), lds, st, \
-                         g, a, lab, class_w, stop);                                                       \
+      hipLaunchKernelGGL((k_mnl_bsp<J_, NW_, NS_, false, false, NB_, RK_>), dim3(grid), dim3(NW_ * TR_WAVE),     \
+                         lds, st, g, a, lab, class_w, stop);                                              \
     return hipGetLastError();
-#define TR_BSP_LAUNCH(J_, NW_, NS_) \
-  if (g.du_nb == 1 && g.du_jt == J_ && g.du_nw == NW_ && g.du_ns == NS_) { TR_BSP_LAUNCH4(J_, NW_, NS_, 1) }
-#define TR_BSP_BLK_LAUNCH(J_, NW_, NS_, NB_) \
-  if (g.du_nb == NB_ && g.du_jt == J_ && g.du_nw == NW_ && g.du_ns == NS_) { TR_BSP_LAUNCH4(J_, NW_, NS_, NB_) }
+#define TR_BSP_LAUNCH(J_, NW_, NS_)                                                                       \
+  if (g.bs_rk == 8 && g.du_nb == 1 && g.du_jt == J_ && g.du_nw == NW_ && g.du_ns == NS_) {                 \
+    TR_BSP_LAUNCH5(J_, NW_, NS_, 1, 8)                                                                    \
+  }
+#define TR_BSP_BLK_LAUNCH(J_, NW_, NS_, NB_)                                                              \
+  if (g.bs_rk == 8 && g.du_nb == NB_ && g.du_jt == J_ && g.du_nw == NW_ && g.du_ns == NS_) {               \
+    TR_BSP_LAUNCH5(J_, NW_, NS_, NB_, 8)                                                                  \
+  }
+#define TR_BSP_R16_LAUNCH(J_, NW_, NS_)                                                                   \
+  if (g.bs_rk == 16 && g.du_nb == 1 && g.du_jt == J_ && g.du_nw == NW_ && g.du_ns == NS_) {                \
+    TR_BSP_LAUNCH5(J_, NW_, NS_, 1, 16)                                                                   \
+  }
     TR_BSP_LIST(TR_BSP_LAUNCH)
     TR_BSP_BLK_LIST(TR_BSP_BLK_LAUNCH)
+    TR_BSP_R16_LIST(TR_BSP_R16_LAUNCH)
     return hipErrorInvalidValue;
 #undef TR_BSP_LAUNCH
 #undef TR_BSP_BLK_LAUNCH
-#undef TR_BSP_LAUNCH4
+#undef TR_BSP_R16_LAUNCH
+#undef TR_BSP_LAUNCH5
   } else if (g.J == 64) {
     hipLaunchKernelGGL((k_mnl_duo<64>), dim3(grid), dim3(DU_T), lds, st, g, a, lab, class_w, stop);
   } else {

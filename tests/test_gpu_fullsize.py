@@ -118,7 +118,7 @@ def test_linear_full_size_vs_fp64(cfg):
 
 
 @pytest.mark.parametrize("form", ["bf16split", "rankblock", "fused", "wide64", "wide256", "wide128x128", "wide512",
-                                  "wide256x128"])
+                                  "wide256x128", "rank16"])
 def test_multinomial_full_size_vs_fp64(form, monkeypatch):
     """Config 3: X (65536, 128, 64), 10 classes, rank 8 (the factored single pass: two 4-wave
     workgroups per CU in the f32 rank-block form (default) and the bf16-split form
@@ -141,6 +141,8 @@ def test_multinomial_full_size_vs_fp64(form, monkeypatch):
     if form == "bf16split":
         monkeypatch.setenv("TR_DUO_SPLIT", "1")
     N, I, J, C, R = 65536, 128, 64, 10, 8
+    if form == "rank16":  # config 3's samples at rank 16: the split body's 16-rank form (round 6)
+        R = 16
     if form.startswith("wide"):
         I, J = (int(form[4:]), 64) if "x" not in form else (int(v) for v in form[4:].split("x"))
         N = 65536 * 128 * 64 // (I * J)
@@ -164,6 +166,8 @@ def test_multinomial_full_size_vs_fp64(form, monkeypatch):
         nb = I // (32 * nw if J == 64 else 16 * nw)
         assert "form=bf16split" in plan.describe and f"waves={nw} " in plan.describe, plan.describe
         assert (f"rowblocks={nb}" in plan.describe) == (nb > 1), plan.describe
+    elif form == "rank16":
+        assert "form=bf16split" in plan.describe and " rk=16" in plan.describe, plan.describe
     elif duo:
         assert f"form={form}" in plan.describe, plan.describe
     cw = np.ones(C, np.float32)

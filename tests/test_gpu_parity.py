@@ -206,8 +206,11 @@ def _multinomial_golden(name, kind="auto"):
     if name.startswith("mnl_bsp") and kind in ("auto", "split"):
         # full-mantissa X of magnitude 1e-3 / 2e-2 on the duo family's shapes: the split body (and at
         # the 32 KiB (64, 128) sample of rank 5 the rank-block body by default)
-        want = "form=bf16split" if kind == "split" or m["rank"] <= 4 else "form=rankblock"
+        # (ranks 9..16: the 16-rank form, 'rk=16')
+        rb = kind == "auto" and 5 <= m["rank"] <= 8 and m["shape"][1] * m["shape"][2] == 8192
+        want = "form=rankblock" if rb else "form=bf16split"
         assert want in plan.describe, plan.describe
+        assert (" rk=16" in plan.describe) == (m["rank"] > 8), plan.describe
     cw, W = mm._class_weights(np.array(m["class_weights"]), dev, yd)
     arena = plan.pack(mm.Bcp)
     grad = torch.zeros(plan.num_grads, device=DEV)
@@ -482,6 +485,15 @@ ROWBLOCK_SHAPES = [((150, 512, 64), 10, 8, 8, 2), ((100, 384, 64), 7, 3, 6, 2), 
                    ((120, 256, 128), 10, 8, 8, 2), ((90, 192, 128), 6, 2, 6, 2), ((70, 288, 128), 3, 7, 6, 3),
                    ((100, 512, 48), 5, 8, 8, 2), ((70, 256, 100), 3, 4, 8, 2), ((7, 256, 128), 3, 8, 8, 2),
                    ((50, 512, 64), 2, 1, 8, 2), ((40, 576, 64), 1, 3, 6, 3), ((60, 192, 100), 4, 6, 6, 2)]
+# (shape, C, rank, waves, nbuf) on the split body's 16-rank form (ranks 9..16, round 6): every wave count
+# at J = 64, the 128-wide shapes, padded rows and widths, config 3's sample shape, one class
+R16_SHAPES = [((300, 64, 64), 10, 12, 2, 2), ((200, 96, 64), 7, 16, 3, 2), ((90, 160, 64), 4, 9, 5, 3),
+              ((60, 224, 64), 3, 13, 7, 2), ((150, 256, 64), 16, 16, 8, 2), ((80, 128, 128), 10, 12, 8, 2),
+              ((120, 96, 128), 6, 16, 6, 2), ((60, 64, 128), 5, 10, 4, 2), ((200, 128, 64), 10, 16, 4, 2),
+              ((300, 100, 64), 10, 11, 4, 2), ((100, 128, 48), 5, 14, 4, 2), ((90, 250, 64), 7, 16, 8, 2),
+              ((120, 192, 64), 1, 15, 6, 3), ((7, 64, 64), 3, 16, 2, 2)]
+# ... and rank 9..16 samples outside it (the padded 128-wide form at 8 waves spills): the two-pass kernels
+R16_OUTSIDE = [((40, 120, 128), 4, 12)]
 # ... and samples above 64 KiB outside them (rows not a whole number of blocks; no spill-free
 # instantiation of their block count): the two-pass kernels
 ROWBLOCK_OUTSIDE = [((40, 300, 128), 4, 8), ((30, 512, 128), 3, 5), ((30, 768, 64), 5, 4)]
@@ -506,6 +518,8 @@ MNL_SHAPES = [((50, 8, 4), 2, 2), ((200, 16, 8), 10, 4), ((97, 5, 7), 16, 3), ((
               *WIDE_SHAPES,
               # ... and as row blocks (samples above 64 KiB: the two-pass kernels before round 6)
               *[r[:3] for r in ROWBLOCK_SHAPES], *ROWBLOCK_OUTSIDE,
+              # ... and at ranks 9..16 (the 16-rank form; k_mnl_fused or two-pass before round 6)
+              *[r[:3] for r in R16_SHAPES], *R16_OUTSIDE,
               # wide classes (C > 16): logits by class tile (MFMA when P % 32 == 0, else VALU),
               # k_softmax_rows, tiled column reduction; rank beyond 64 (MTTKRP rank tiles)
               ((150, 8, 4), 17, 3), ((230, 16, 8), 40, 5), ((99, 5, 7), 33, 2), ((200, 12), 100, 4),
@@ -550,6 +564,22 @@ def test_multinomial_row_blocks_selected(shape, C, rank, nw, nb):
     with path("auto"):
         desc = _multinomial_sweep(shape, C, rank)
     assert "form=bf16split" in desc and f"waves={nw} wg/cu=1 nbuf=2 " in desc and f"rowblocks={nb}" in desc, desc
+
+
+@pytest.mark.parametrize("shape,C,rank,nw,nbuf", R16_SHAPES)
+def test_multinomial_rank16_form_selected(shape, C, rank, nw, nbuf):
+    """Ranks 9..16 take the split body's 16-rank form ('rk=16') on its shapes by default; the results are
+    the sweep's (test_multinomial_sweep_vs_oracle runs every kind on these shapes)."""
+    with path("auto"):
+        desc = _multinomial_sweep(shape, C, rank)
+    assert "form=bf16split" in desc and " rk=16" in desc and f"waves={nw} wg/cu={8 // nw} nbuf={nbuf} " in desc, desc
+
+
+@pytest.mark.parametrize("shape,C,rank", R16_OUTSIDE)
+def test_multinomial_rank16_outside(shape, C, rank):
+    with path("auto"):
+        desc = _multinomial_sweep(shape, C, rank)
+    assert " duo " not in desc, desc
 
 
 @pytest.mark.parametrize("shape,C,rank", ROWBLOCK_OUTSIDE)
@@ -599,7 +629,8 @@ SPLIT_SCALE_SHAPES = [((300, 64, 64), 10, 8, "auto"), ((200, 96, 64), 7, 3, "aut
                       ((120, 96, 128), 6, 7, "auto"), ((80, 128, 128), 10, 8, "auto"),
                       ((300, 100, 64), 10, 8, "auto"), ((200, 128, 48), 10, 8, "auto"), ((80, 70, 128), 4, 8, "auto"),
                       ((256, 128, 64), 10, 3, "auto"), ((256, 128, 64), 10, 8, "split"),
-                      ((64, 256, 128), 10, 8, "auto"), ((40, 512, 64), 7, 5, "auto")]
+                      ((64, 256, 128), 10, 8, "auto"), ((40, 512, 64), 7, 5, "auto"),
+                      ((256, 128, 64), 10, 16, "auto"), ((150, 96, 128), 6, 12, "auto")]
 
 
 @pytest.mark.parametrize("xscale", [1e-4, 1e-2, 1.0, 1e4, 3e7, "mixed"])

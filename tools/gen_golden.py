@@ -495,6 +495,12 @@ def main():
              {'lr': 0.01}, 40, x_scale=1e-3)
     mnl_case("mnl_bsp_f32x_j128", 49, (16, 64, 128), 6, 5, [False, False, False], [1.0] * 6, 0.01,
              {'lr': 0.01, 'amsgrad': True}, 30, x_scale=2e-2)
+    # ranks 9..16 on the split body's 16-rank form (round 6): (96, 64) rank 12 (three 32-row waves,
+    # a non-negative mode) and config 3's sample shape at rank 16
+    mnl_case("mnl_bsp_r16_w3", 50, (40, 96, 64), 7, 12, [False, True, False], [1.0, 0.5, 2.0, 1.5, 1.0, 0.8, 1.2],
+             0.01, {'lr': 0.01}, 30)
+    mnl_case("mnl_bsp_r16_c3", 51, (24, 128, 64), 10, 16, [False, False, False], [1.0] * 10, 0.01,
+             {'lr': 0.01, 'amsgrad': True}, 30)
     init_case("init_rng")
     spectral_case("spec_basic", 31, (64, 12, 9), 3, 2, 2, 1, False, 0.01, adam, 50)
     spectral_case("spec_nonneg_amsgrad_wd", 32, (80, 16, 17), 2, 3, 2, 2, [True, False, True], 0.02,
