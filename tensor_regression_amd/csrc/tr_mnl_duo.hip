@@ -26,7 +26,8 @@
 // body at those shapes rank <= 4 and at every (32 NW, 64) sample (NW = 2..8) and (16 NW, 128)
 // sample (NW = 4, 6, 8) rank <= 8, any other I <= 256 / <= 128 and J % 4 == 0 in 28..128
 // padded to the next of those shapes when it fills a third of it; taller samples whose rows are 2 or 3
-// such blocks (NW = 8 or 6) streamed through the ring one row block per slot; <= 16 classes.  Other two-mode
+// such blocks (NW = 8 or 6) streamed through the ring one row block per slot; ranks 9..16 in a 16-rank
+// form of the split body (RK = 16); <= 16 classes.  Other two-mode
 // shapes run k_mnl_fused (tr_mnl.hip) where it fits and the sample is >= 24 KiB, else the two-pass
 // kernels (DESIGN.md "Multinomial, round 5").
 //
