@@ -17,6 +17,8 @@
 // summed in index order by k_reduce_slabs (+ softplus chain): bitwise reproducible.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "tr_common.h"
 #include "tr_spectral.h"
 
@@ -82,6 +84,94 @@ __global__ __launch_bounds__(256) void k_specg_fwd(const float* __restrict__ X, 
           const int dd = dt * 16 + 4 * q + r;
           if (dd < D) tn[(int64_t)dd * KP + t * 16 + i] = acc[t][r];
         }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// forward, vectorised (round 6; K <= 64): T^T = Phi0^T X_n on v_mfma_f32_16x16x4_f32 with the d
+// columns as N.  Wave wv of d group blockIdx.x owns d in [256 dg + 64 wv, +64); per 4 w rows, lane
+// (i, q) reads X[w0 + q][d0 + 4i .. 4i + 3] as ONE 16-B buffer load (any D: 4-B aligned dwordx4s
+// read exactly, tools/buf_range_probe.hip; rows past W come back zero from the sample's buffer
+// range, and a quad straddling D reads the next row's first values, masked here) and MFMA m of the
+// four takes component m: A = Phi0[w0 + q][k0 + i], B = X[w0 + q][d0 + 4i + m], so C[k][i] of MFMA m
+// is T[d0 + 4i + m][k] -- lane (i, q) holds four consecutive k of one d: one 16-B store.  (The
+// scalar form above reads 4 B per lane and instruction: 26 % of HBM at (512, 129).)
+// ------------------------------------------------------------------------------------------
+template <int KTM>
+__global__ __launch_bounds__(64) void k_specg_fwd4(const float* __restrict__ X, int64_t N, int64_t xld, SpecGeom g,
+                                                    const float* __restrict__ Phi0, float* __restrict__ T,
+                                                    int64_t rows_per_blk, const int32_t* __restrict__ stop) {
+  if (stop != nullptr && *stop != 0) return;
+  // (one wave per workgroup: d group blockIdx.x of 64 columns, sample block blockIdx.y)
+  const int lane = threadIdx.x & 63;
+  const int W = g.W, D = g.D, K = g.K, KP = g.gKP;  // (KP == 16 KTM: the launch's choice)
+  const int i = lane & 15, q = lane >> 4;
+  const int d0 = blockIdx.x * 64;
+  const int db = d0 + 4 * i;  // this lane's quad of d
+  bool mok[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) mok[m] = db + m < D;
+  const int64_t n0 = (int64_t)blockIdx.y * rows_per_blk;
+  const int64_t n1 = n0 + rows_per_blk < N ? n0 + rows_per_blk : N;
+  const __amdgpu_buffer_rsrc_t prs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)Phi0, (short)0, (int)((int64_t)W * K * 4), 0x00020000);
+  for (int64_t n = n0; n < n1; ++n) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(uintptr_t)(X + n * xld), (short)0, (int)((int64_t)W * D * 4), 0x00020000);
+    sg_f32x4 acc[KTM][4];
+#pragma unroll
+    for (int t = 0; t < KTM; ++t)
+#pragma unroll
+      for (int m = 0; m < 4; ++m) acc[t][m] = sg_f32x4{0.f, 0.f, 0.f, 0.f};
+    // SG_U steps of 4 rows per batch, the next batch's loads issued before this batch's MFMAs: one
+    // load in flight per wave left the loop waiting on memory latency (1.09 ms at (512, 129))
+    constexpr int SG_U = 4;
+    const int xvo = 4 * (q * D + db), pvo = 4 * (q * K + i);
+    bool kok[KTM];  // column k = 16 t + i of Phi0 exists (past K: the next row's values, masked)
+#pragma unroll
+    for (int t = 0; t < KTM; ++t) kok[t] = 16 * t + i < K;
+    sg_f32x4 xb[2][SG_U];
+    float ab[2][SG_U][KTM];
+    // (per-lane offsets fixed, the row in the scalar offset: no per-element address registers; rows
+    // past W read zeros from both buffers' ranges, columns k >= K of Phi0 are masked)
+    auto load_batch = [&](int w0, int buf) {
+#pragma unroll
+      for (int u = 0; u < SG_U; ++u) {
+        const int wr = w0 + 4 * u;
+        xb[buf][u] = __builtin_bit_cast(sg_f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, xvo, 4 * wr * D, 0));
+#pragma unroll
+        for (int t = 0; t < KTM; ++t)  // (loaded unconditionally, masked by a select: a conditional
+          // load compiles to a branch with a vmcnt(0) wait inside it, which serialised the loop)
+          ab[buf][u][t] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(prs, pvo, 4 * (wr * K + 16 * t), 0));
+      }
+    };
+    auto compute = [&](int buf) {  // (called with a literal: the buffer index is compile-time)
+#pragma unroll
+      for (int u = 0; u < SG_U; ++u)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          if (d0 + m >= D) continue;  // (uniform: no lane's column d0 + 4 i + m exists; D = 129's tail)
+          const float b = mok[m] ? xb[buf][u][m] : 0.f;
+#pragma unroll
+          for (int t = 0; t < KTM; ++t) acc[t][m] = sg_mfma(kok[t] ? ab[buf][u][t] : 0.f, b, acc[t][m]);
+        }
+    };
+    const int nbat = (W + 4 * SG_U - 1) / (4 * SG_U);
+    load_batch(0, 0);
+    for (int bt = 0; bt < nbat; bt += 2) {
+      if (bt + 1 < nbat) load_batch((bt + 1) * 4 * SG_U, 1);
+      compute(0);
+      if (bt + 1 < nbat) {
+        if (bt + 2 < nbat) load_batch((bt + 2) * 4 * SG_U, 0);
+        compute(1);
+      }
+    }
+    float* tn = T + n * (int64_t)D * KP;
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+      if (mok[m])
+#pragma unroll
+        for (int t = 0; t < KTM; ++t) *reinterpret_cast<sg_f32x4*>(tn + (int64_t)(db + m) * KP + t * 16 + 4 * q) = acc[t][m];
   }
 }
 
@@ -334,6 +424,102 @@ __global__ __launch_bounds__(256) void k_specg_bwd(const float* __restrict__ X, 
       }
 }
 
+// backward, batched (round 6): k_specg_bwd's MFMA layout, every operand by buffer load at a fixed
+// per-lane offset with the d step in the scalar offset (X: one 16-B load per lane and step, any D;
+// dT: the sample's D x KP image, rows past D read zero), SG_UB steps per batch and the next batch's
+// loads issued before this batch's MFMAs.
+template <int KTM>
+__global__ __launch_bounds__(256) void k_specg_bwd4(const float* __restrict__ X, int64_t N, int64_t xld, SpecGeom g,
+                                                    const float* __restrict__ T, float* __restrict__ slab,
+                                                    int64_t slab_stride, int64_t rows_per_blk,
+                                                    const int32_t* __restrict__ stop) {
+  if (stop != nullptr && *stop != 0) return;
+  // two 16-row w tiles per wave (each dT operand feeds both): wave wv of w group blockIdx.x owns
+  // rows [128 blockIdx.x + 32 wv, +32)
+  constexpr int SG_UB = 4, NWT = 2;
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int W = g.W, D = g.D, K = g.K, KP = g.gKP, Rn = g.Rn, Rs = g.Rs, Cc = g.Cc;  // (KP == 16 KTM)
+  const int w00 = blockIdx.x * 128 + wv * 32;
+  const int i = lane & 15, q = lane >> 4;
+  const int64_t n0 = (int64_t)blockIdx.y * rows_per_blk;
+  const int64_t n1 = n0 + rows_per_blk < N ? n0 + rows_per_blk : N;
+  sg_f32x4 acc[NWT][KTM];
+#pragma unroll
+  for (int h = 0; h < NWT; ++h)
+#pragma unroll
+    for (int tt = 0; tt < KTM; ++tt) acc[h][tt] = sg_f32x4{0.f, 0.f, 0.f, 0.f};
+  int xvo[NWT];  // rows past W: out of range, zero
+#pragma unroll
+  for (int h = 0; h < NWT; ++h) {
+    const int w = w00 + 16 * h + i;
+    xvo[h] = w < W ? 4 * (w * D + 4 * q) : 0x40000000;
+  }
+  const int tvo = 4 * (4 * q * KP + i);
+  const int nds = (D + 15) / 16;
+  if (w00 < W) {
+    for (int64_t n = n0; n < n1; ++n) {
+      const __amdgpu_buffer_rsrc_t xs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(uintptr_t)(X + n * xld), (short)0, (int)((int64_t)W * D * 4), 0x00020000);
+      const __amdgpu_buffer_rsrc_t ts = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(uintptr_t)(T + n * (int64_t)D * KP), (short)0, (int)((int64_t)D * KP * 4), 0x00020000);
+      sg_f32x4 xb[2][SG_UB][NWT];
+      float bb[2][SG_UB][4][KTM];
+      auto load_batch = [&](int s0, int buf) {
+#pragma unroll
+        for (int u = 0; u < SG_UB; ++u) {
+          const int d0 = 16 * (s0 + u);
+#pragma unroll
+          for (int h = 0; h < NWT; ++h)
+            xb[buf][u][h] = __builtin_bit_cast(sg_f32x4, __builtin_amdgcn_raw_buffer_load_b128(xs, xvo[h], 4 * d0, 0));
+#pragma unroll
+          for (int m = 0; m < 4; ++m)
+#pragma unroll
+            for (int tt = 0; tt < KTM; ++tt)
+              bb[buf][u][m][tt] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ts, tvo, 4 * ((d0 + m) * KP + 16 * tt), 0));
+        }
+      };
+      auto compute = [&](int s0, int buf) {
+#pragma unroll
+        for (int u = 0; u < SG_UB; ++u) {
+          const int db = 16 * (s0 + u) + 4 * q;
+#pragma unroll
+          for (int m = 0; m < 4; ++m)
+#pragma unroll
+            for (int h = 0; h < NWT; ++h) {
+              const float a = db + m < D ? xb[buf][u][h][m] : 0.f;  // (a quad straddling D: the next row's values)
+#pragma unroll
+              for (int tt = 0; tt < KTM; ++tt) acc[h][tt] = sg_mfma(a, bb[buf][u][m][tt], acc[h][tt]);
+            }
+        }
+      };
+      load_batch(0, 0);
+      for (int s0 = 0; s0 < nds; s0 += 2 * SG_UB) {
+        if (s0 + SG_UB < nds) load_batch(s0 + SG_UB, 1);
+        compute(s0, 0);
+        if (s0 + SG_UB < nds) {
+          if (s0 + 2 * SG_UB < nds) load_batch(s0 + 2 * SG_UB, 0);
+          compute(s0 + SG_UB, 1);
+        }
+      }
+    }
+  }
+  if (w00 >= W) return;
+  float* sl = slab + (int64_t)blockIdx.y * slab_stride;
+#pragma unroll
+  for (int h = 0; h < NWT; ++h)
+#pragma unroll
+    for (int tt = 0; tt < KTM; ++tt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ww = w00 + 16 * h + 4 * q + r, k = tt * 16 + i;
+        if (ww < W && k < K) {
+          const int64_t dst = k < Rn ? g.offA0 + (int64_t)ww * Rn + k : g.offC0 + (int64_t)ww * Rs * Cc + (k - Rn);
+          sl[dst] = acc[h][tt][r];
+        }
+      }
+}
+
 // ------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------
@@ -371,7 +557,26 @@ hipError_t launch_specg(int mode, const SpecGeom& g, int nchunks, const float* X
   if (N < 1 || nchunks < 1) return hipSuccess;
   const int64_t rpb = (N + nchunks - 1) / nchunks;
   const unsigned nblk = (unsigned)((N + rpb - 1) / rpb);
-  {
+  static const bool scalar_fwd = [] {  // TR_SPECG_SCALAR=1: the round-1 scalar forward (A/B)
+    const char* v = std::getenv("TR_SPECG_SCALAR");
+    return v != nullptr && v[0] == '1';
+  }();
+  if (g.gKP <= 64 && !scalar_fwd) {
+    // (its own sample blocks: it writes no slabs; about 8 waves per CU per d group; the k tile count
+    // compiled in)
+    const int64_t rpf = (N + 4095) / 4096;
+    const dim3 grid((unsigned)((g.D + 63) / 64), (unsigned)((N + rpf - 1) / rpf));
+#define SG_F4(KM) hipLaunchKernelGGL((k_specg_fwd4<KM>), grid, dim3(64), 0, st, X, N, xld, g, Phi0, T, rpf, stop)
+    switch (g.gKP / 16) {
+      case 1: SG_F4(1); break;
+      case 2: SG_F4(2); break;
+      case 3: SG_F4(3); break;
+      default: SG_F4(4); break;
+    }
+#undef SG_F4
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  } else {
     const dim3 grid((unsigned)((g.D + 63) / 64), nblk);
 #define SG_FWD(KM) hipLaunchKernelGGL((k_specg_fwd<KM>), grid, dim3(256), 0, st, X, N, xld, g, Phi0, T, rpb, stop)
     SG_KT_CASES(SG_FWD)
@@ -398,6 +603,19 @@ hipError_t launch_specg(int mode, const SpecGeom& g, int nchunks, const float* X
     hipLaunchKernelGGL((k_specg_bwd<KM, 1>), grid, dim3(256), 0, st, X, N, xld, g, T, slab, slab_stride, rpb, stop); \
   else                                                                                                          \
     hipLaunchKernelGGL((k_specg_bwd<KM, 0>), grid, dim3(256), 0, st, X, N, xld, g, T, slab, slab_stride, rpb, stop)
+  if (g.gKP <= 64 && !scalar_fwd) {
+    const dim3 grid4((unsigned)((g.W + 127) / 128), nblk);
+#define SG_B4(KM) \
+  hipLaunchKernelGGL((k_specg_bwd4<KM>), grid4, dim3(256), 0, st, X, N, xld, g, T, slab, slab_stride, rpb, stop)
+    switch (g.gKP / 16) {
+      case 1: SG_B4(1); break;
+      case 2: SG_B4(2); break;
+      case 3: SG_B4(3); break;
+      default: SG_B4(4); break;
+    }
+#undef SG_B4
+    return hipGetLastError();
+  }
   SG_KT_CASES(SG_BWD)
 #undef SG_BWD
   return hipGetLastError();
