@@ -13,7 +13,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TR_HIP_LIB", os.path.join(_HERE, "libtr_hip.so"))
 
-TR_ABI_VERSION = 7
+TR_ABI_VERSION = 8
 TR_STOP_DEVICE_ERROR = -(1 << 30)
 TR_MODEL_LINEAR = 0
 TR_MODEL_MULTINOMIAL = 1
@@ -50,6 +50,7 @@ SIGNATURES = {
     "tr_spectral_latents": (_c.c_int, [_vp, _vp, _c.c_int64, _vp, _vp, _vp]),
     "tr_plan_set_x_stride": (_c.c_int, [_vp, _c.c_int64]),
     "tr_x_range": (_c.c_int, [_vp, _c.c_int64, _c.c_int64, _c.c_int64, _vp, _c.c_int, _vp]),
+    "tr_mnl_geometry": (_c.c_int, [_c.c_int64, _c.c_int64, _c.c_int, _c.c_int, _vp, _c.c_int]),
     "tr_plan_set_x_range": (_c.c_int, [_vp, _c.c_double, _c.c_double, _c.c_double]),
     "tr_plan_status": (_c.c_int, [_vp, _c.POINTER(_c.c_int32)]),
     "tr_adam_step": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _c.c_float, _c.c_double, _c.c_double,

@@ -244,3 +244,77 @@ def test_watchdog_counts_time_without_progress():
     errs = iter([None, None, "remote process exited"])
     with pytest.raises(_CollectiveError, match="remote process"):
         wait_progress([_FakeEvent(clk, 1e9)], lambda: next(errs), 1e6, clock=clk, sleep=clk.sleep)
+
+
+def _mnl_geometry(I, J, R, C=10):
+    from tensor_regression_amd import _lib
+    lib = _lib.load()
+    out = (ctypes.c_int32 * 11)()
+    rc = lib.tr_mnl_geometry(I, J, R, C, out, 11)
+    keys = ["duo", "bsp", "waves", "wg_per_cu", "ring", "padded", "row_width", "row_blocks", "rank_cols",
+            "lds_bytes", "fused_ok"]
+    return rc, dict(zip(keys, list(out)))
+
+
+# (I, J, R): expected (duo, bsp, waves, wg/CU, ring, padded, row width, row blocks, rank columns);
+# the multinomial factored pass's envelope as DESIGN.md "Multinomial" describes it (no device needed:
+# the plan may still fall back at creation when an instantiation spills)
+MNL_GEOMETRY = [
+    ((128, 64, 8), (1, 0, 4, 2, 2, 0, 64, 1, 8)),      # config 3: rank-block body
+    ((128, 64, 3), (1, 1, 4, 2, 2, 0, 64, 1, 8)),      # rank <= 4: split body
+    ((128, 64, 16), (1, 1, 4, 2, 2, 0, 64, 1, 16)),    # ranks 9..16: the 16-rank form
+    ((64, 64, 8), (1, 1, 2, 4, 2, 0, 64, 1, 8)),
+    ((160, 64, 8), (1, 1, 5, 1, 3, 0, 64, 1, 8)),      # ring of three at 5 / 6 waves
+    ((96, 128, 12), (1, 1, 6, 1, 2, 0, 128, 1, 16)),   # (no ring of three for the 128-wide 16-rank form)
+    ((100, 64, 8), (1, 1, 4, 2, 2, 1, 64, 1, 8)),      # padded rows
+    ((128, 48, 8), (1, 1, 4, 2, 2, 1, 64, 1, 8)),      # padded width
+    ((512, 64, 8), (1, 1, 8, 1, 2, 0, 64, 2, 8)),      # row blocks
+    ((256, 128, 8), (1, 1, 8, 1, 2, 0, 128, 2, 8)),
+    ((384, 64, 5), (1, 1, 6, 1, 2, 0, 64, 2, 8)),
+    ((288, 128, 8), (1, 1, 6, 1, 2, 0, 128, 3, 8)),
+    ((512, 48, 8), (1, 1, 8, 1, 2, 1, 64, 2, 8)),
+]
+MNL_GEOMETRY_OUTSIDE = [(768, 64, 8), (300, 128, 8), (512, 128, 8), (256, 128, 12), (16, 64, 8), (64, 24, 8),
+                        (128, 64, 17)]
+
+
+@pytest.mark.parametrize("shape,want", MNL_GEOMETRY)
+def test_mnl_geometry_envelope(shape, want, monkeypatch):
+    for k in ("TR_MNL_DUO", "TR_DUO_SPLIT", "TR_DUO_ANYFILL"):
+        monkeypatch.delenv(k, raising=False)
+    rc, g = _mnl_geometry(*shape)
+    assert rc == 0
+    got = tuple(g[k] for k in ["duo", "bsp", "waves", "wg_per_cu", "ring", "padded", "row_width", "row_blocks",
+                               "rank_cols"])
+    assert got == want, g
+    assert g["wg_per_cu"] * g["lds_bytes"] <= 160 * 1024, g
+
+
+@pytest.mark.parametrize("shape", MNL_GEOMETRY_OUTSIDE)
+def test_mnl_geometry_outside(shape, monkeypatch):
+    """Outside the family: rows not whole blocks or four blocks (768, 64), (512, 128); rank > 8 with
+    row blocks; a sample filling less than a third of its padded shape; J < 28; rank > 16."""
+    for k in ("TR_MNL_DUO", "TR_DUO_SPLIT", "TR_DUO_ANYFILL"):
+        monkeypatch.delenv(k, raising=False)
+    rc, g = _mnl_geometry(*shape)
+    assert rc == 0 and g["duo"] == 0, g
+
+
+def test_mnl_geometry_switches(monkeypatch):
+    for k in ("TR_MNL_DUO", "TR_DUO_SPLIT", "TR_DUO_ANYFILL"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("TR_DUO_SPLIT", "1")  # the split body at config 3's rank 8
+    assert _mnl_geometry(128, 64, 8)[1]["bsp"] == 1
+    monkeypatch.setenv("TR_DUO_SPLIT", "0")  # the rank-block body only
+    assert _mnl_geometry(128, 64, 8)[1]["bsp"] == 0 and _mnl_geometry(64, 64, 8)[1]["duo"] == 0
+    monkeypatch.delenv("TR_DUO_SPLIT")
+    monkeypatch.setenv("TR_DUO_ANYFILL", "1")  # any fill of the padded shape (the tests' switch)
+    assert _mnl_geometry(16, 64, 8)[1]["duo"] == 1
+    monkeypatch.delenv("TR_DUO_ANYFILL")
+    monkeypatch.setenv("TR_MNL_DUO", "0")
+    assert _mnl_geometry(128, 64, 8)[1]["duo"] == 0
+    from tensor_regression_amd import _lib
+    lib = _lib.load()
+    out = (ctypes.c_int32 * 11)()
+    assert lib.tr_mnl_geometry(128, 64, 40, 10, out, 11) == -2  # rank beyond the factored kernels
+    assert lib.tr_mnl_geometry(128, 64, 8, 10, None, 11) == -1
