@@ -13,7 +13,10 @@
 //                 float4 feeding four k steps) -> the A0 / C0 entries of the same slabs
 //
 // X crosses HBM twice per iteration (k_specg_fwd, k_specg_bwd) plus T / dT (D*Kp per sample):
-// the fallback trades the fused kernel's single pass for an unbounded sample shape.  Slabs are
+// the fallback trades the fused kernel's single pass for an unbounded sample shape.  For Kp <= 64
+// (round 6) the forward and backward run k_specg_fwd4 / k_specg_bwd4: 16-B buffer loads at fixed
+// per-lane offsets, the k tile count compiled in (no conditional operand loads), batched loads
+// issued a batch ahead (1.7x the round-1 kernels at (512, 129); TR_SPECG_SCALAR=1 keeps those).  Slabs are
 // summed in index order by k_reduce_slabs (+ softplus chain): bitwise reproducible.
 #include <hip/hip_runtime.h>
 
