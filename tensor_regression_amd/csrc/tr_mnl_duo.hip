@@ -561,7 +561,7 @@ __device__ __forceinline__ void duo_body(const MnlGeom& g, const DuArgs& a, cons
 // U partial over its rows goes through LDS: NW partials per sample); V is a partial over the
 // wave's i k-step, and dPhi1 = sum_n Wv_n V_n is linear in it: the waves' partials are summed
 // once, at the end.  Every wave runs the softmax epilogue of the previous sample (staged between
-// its GEMM steps) for all 8 ranks; wave 0 alone accumulates dPhiC and the loss.
+// its GEMM steps) for all ranks; wave 0 alone accumulates dPhiC and the loss.
 template <int... T, class F>
 __device__ __forceinline__ void for_each_ic(std::integer_sequence<int, T...>, F&& f) {
   (f(std::integral_constant<int, T>()), ...);
@@ -784,8 +784,8 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
   int64_t yP = 0;
   float cwP = 0.f;
 
-  // ---- epilogue of one sample in 8 stages (duo_body's chain, all 8 ranks: row gq carries ranks
-  // gq and gq + 4) ----
+  // ---- epilogue of one sample in 8 stages (duo_body's chain, every rank: DPP row gq carries ranks
+  // gq + 4 k, k < RK / 4) ----
   // (the stages' values, one instance per epilogue: an instance shared across iterations would be
   // carried around the BLK loop, whose stages run only in a sample's first block)
   struct EpiSt {
