@@ -501,6 +501,12 @@ def main():
              0.01, {'lr': 0.01}, 30)
     mnl_case("mnl_bsp_r16_c3", 51, (24, 128, 64), 10, 16, [False, False, False], [1.0] * 10, 0.01,
              {'lr': 0.01, 'amsgrad': True}, 30)
+    # samples above 64 KiB on the split body's row blocks (round 6): (512, 64) as two (256, 64)
+    # blocks, (256, 128) as two (128, 128) blocks with full-mantissa X
+    mnl_case("mnl_bsp_rowblk_512x64", 52, (10, 512, 64), 5, 6, [False, False, False], [1.0, 2.0, 0.5, 1.0, 1.5],
+             0.01, {'lr': 0.01}, 30)
+    mnl_case("mnl_bsp_rowblk_256x128", 53, (8, 256, 128), 4, 8, [True, False, False], [1.0] * 4, 0.01,
+             {'lr': 0.005}, 30, x_scale=2e-2)
     init_case("init_rng")
     spectral_case("spec_basic", 31, (64, 12, 9), 3, 2, 2, 1, False, 0.01, adam, 50)
     spectral_case("spec_nonneg_amsgrad_wd", 32, (80, 16, 17), 2, 3, 2, 2, [True, False, True], 0.02,
