@@ -573,11 +573,24 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
   const int t = threadIdx.x;
   // J = 64: NW waves, each owning 32 rows of a (32 NW, 64) sample; J = 128: NW waves over a
   // (16 NW, 128) sample, each owning 16 T rows and one (32-row k-step, 16-chunk group) of V
-  constexpr int J = JT, I = JT == 64 ? 32 * NW : 16 * NW, SPF = I * J, JQ = J / 4, NT_ = NW * TR_WAVE;
-  static_assert(JT == 64 || NW % 2 == 0, "J = 128: two chunk groups per V k-step");
-  constexpr int NT = JT == 64 ? 2 : 1;  // T i-tiles per wave
-  constexpr int NKS = I / 32;           // V k-steps (J = 128: NW / 2 of them, two chunk groups each)
+  // (J = 32: NW waves over a (32 NW, 32) sample, each owning 32 T rows and one V k-step of 32
+  // rows; see J32 below)
+  constexpr bool J32 = JT == 32;
+  constexpr int J = JT, I = JT == 128 ? 16 * NW : 32 * NW, SPF = I * J, JQ = J / 4, NT_ = NW * TR_WAVE;
+  static_assert(JT != 128 || NW % 2 == 0, "J = 128: two chunk groups per V k-step");
+  constexpr int NT = JT == 128 ? 1 : 2;  // T i-tiles per wave
+  constexpr int NKS = I / 32;            // V k-steps (J = 128: NW / 2 of them, two chunk groups each)
   constexpr int NKT = J / 32;  // T k-steps (j)
+  // J = 32: V's 32 columns are two j-tiles of 16 (tile t: lane n's column j = 4 (n & 7) + t +
+  // 2 (n >> 3), lanes n and n + 8 read one chunk), one V k-step's 32 rows are ordered i = iv0 +
+  // 4 e + gq (lane groups gq, gq + 1 on rows of both parities: conflict-free chunk reads), and the
+  // 128-byte rows take the chunk swizzle q ^ ((i / 2 + 2) & 7) (T's 16-lane read groups cover the 16
+  // (row parity, chunk slot) pairs)
+  constexpr int NVS = J32 ? 2 : 4;  // V steps (j-tiles)
+  constexpr int NG = SPF / (NW * 256);  // 1 KiB LDS-DMA pieces per wave per sample (8; J = 32: 4)
+  static_assert(NG == NT * NKT + NVS, "one LDS-DMA piece per GEMM step");
+  static_assert(!J32 || (NB == 1 && RK == 8), "J = 32: one block, 8 rank columns");
+  auto swz = [](int i) { return J32 ? ((i >> 1) + 2) & 7 : i & 15; };
   const int R = g.R, C = g.C;
   // PAD: the sample's g.I x g.J (g.J % 4 == 0) fills only part of the compiled I x J; the padding
   // rows and column chunks read the sample's first chunk (valid memory) and meet zero Phi0 / Phi1 rows
@@ -615,8 +628,9 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
   const float NEG = -__builtin_huge_valf();
 
   const int it0 = NT == 2 ? 32 * wv : 16 * wv;                    // first T row of this wave
-  const int iv0 = JT == 64 ? 32 * wv : 32 * (wv % NKS);           // V k-step (rows) of this wave
-  const int cv = n + (J == 128 ? 16 * (wv / NKS) : 0);            // V chunk (j = 4 cv + tile)
+  const int iv0 = JT == 128 ? 32 * (wv % NKS) : 32 * wv;          // V k-step (rows) of this wave
+  const int cv = J32 ? (n & 7) : n + (J == 128 ? 16 * (wv / NKS) : 0);  // V chunk (j = 4 cv + tile)
+  auto vrow = [&](int e) { return J32 ? iv0 + 4 * e + gq : iv0 + 8 * gq + e; };  // V element e's row
   // B operands, split once per launch: T (Phi1, element e of lane group gq <-> j = 32 s + 8 gq + e)
   // (RK = 16: bT12 / bV12 hold b1, bT2 / bV2 b2, bT3 / bV3 b3, hT / hV f16(x))
   constexpr int N2 = R16 ? NKT : 1;
@@ -652,7 +666,7 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
              (rok && (!PAD || j + 1 < Jr)) ? P1[(int64_t)(j + 1) * R + r8] : 0.f, bT12[s][v], bT2[R16 ? s : 0][v],
              bT3[s][v], hT[s][v]);
     }
-  // V (Phi0, element e <-> i = iv0 + 8 gq + e) and the U weights: T accumulator (lane (n, gq), reg
+  // V (Phi0, element e <-> i = vrow(e)) and the U weights: T accumulator (lane (n, gq), reg
   // v) = T[it0 + 16 tt + 4 gq + v][n & 7] after the column fold; lanes n >= 8 hold the same values
   // and weigh 0.  Both depend on the row block: BLK loads the raw Phi0 values of the next block at
   // the end of a block (they land with that block's LDS-DMA wait) and splits them after its barrier
@@ -677,7 +691,7 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
     } else {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const int i = iv0 + 8 * gq + e;
+        const int i = vrow(e);
         pvr[e] = (rok && (!PAD || i < Ir)) ? P0[(int64_t)i * R + r8] : 0.f;
       }
 #pragma unroll
@@ -700,10 +714,10 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
   };
   load_rows(0, phiU);
   if constexpr (!BLK) split_rows();
-  // epilogue weights: pc[r] = w_r PhiC[c][r]; row gq's ranks gq + 4 k.  BLK and RK = 16 read them
+  // epilogue weights: pc[r] = w_r PhiC[c][r]; row gq's ranks gq + 4 k.  BLK, RK = 16 and J = 32 read them
   // from an LDS table in the rank-block body's Phi1 slots (unused here) in the epilogue: those forms
   // need the registers
-  constexpr bool PCL = BLK || R16;  // pc[] from the LDS table
+  constexpr bool PCL = BLK || R16 || J32;  // pc[] from the LDS table (J = 32: three waves per SIMD)
   float pc[8];
 #pragma unroll
   for (int r = 0; r < 8; ++r) pc[r] = (!PCL && cok && r < R) ? a.w[r] * PC[c * R + r] : 0.f;
@@ -732,30 +746,30 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
     for (int e = t; e < 2 * tbn; e += NT_) sTB[e] = 0.f;
 
   // LDS-DMA map (as the rank-block form): wave wv issues the 1 KiB groups wv + NW gi of every sample
-  uint32_t goff[8];
+  uint32_t goff[NG];
 #pragma unroll
-  for (int gi = 0; gi < 8; ++gi) {
+  for (int gi = 0; gi < NG; ++gi) {
     const int slot = (wv + NW * gi) * TR_WAVE + lane;
     const int i = slot / JQ;
     const int q = slot - i * JQ;
     if (PAD) {  // source offset in the real (Ir x Jr) sample; padding: its first chunk
-      const int cq = q ^ (i & 15);
+      const int cq = q ^ swz(i);
       goff[gi] = (i < Ir && 4 * cq < Jr) ? 4u * (uint32_t)(i * Jr + 4 * cq) : 0u;
     } else {
-      goff[gi] = 4u * (uint32_t)(i * J + 4 * (q ^ (i & 15)));
+      goff[gi] = 4u * (uint32_t)(i * J + 4 * (q ^ swz(i)));
     }
   }
   const uint32_t lbase = (uint32_t)__builtin_amdgcn_readfirstlane(
       (int)(uint32_t)(uintptr_t)((const __attribute__((address_space(3))) float*)lds));
-  // LDS read offsets (floats): T row it0 + 16 tt + n, chunks 8 s + 2 gq (+1); V rows iv0 + 8 gq + e, chunk cv
+  // LDS read offsets (floats): T row it0 + 16 tt + n, chunks 8 s + 2 gq (+1); V rows vrow(e), chunk cv
   int tro[NT], vro[8];
 #pragma unroll
   for (int tt = 0; tt < NT; ++tt) tro[tt] = (it0 + 16 * tt + n) * J;
-  const int tsw = n;  // (it0 + 16 tt + n) & 15 = n
+  const int tsw = swz(n);  // swz(it0 + 16 tt + n) = swz(n)
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    const int i = iv0 + 8 * gq + e;
-    vro[e] = i * J + 4 * (cv ^ (i & 15));
+    const int i = vrow(e);
+    vro[e] = i * J + 4 * (cv ^ swz(i));
   }
 
   const int64_t n0 = (int64_t)blockIdx.x * a.rows_per_wg;
@@ -767,20 +781,20 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
   __syncthreads();
   __builtin_amdgcn_s_waitcnt(0);
 
-  du_f32x4 gT[NT], gV[4];  // dPhi0 rows of this wave's T tiles, dPhi1 partial of its V tiles
+  du_f32x4 gT[NT], gV[NVS];  // dPhi0 rows of this wave's T tiles, dPhi1 partial of its V tiles
 #pragma unroll
   for (int q = 0; q < NT; ++q) gT[q] = du_f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int q = 0; q < 4; ++q) gV[q] = du_f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int q = 0; q < NVS; ++q) gV[q] = du_f32x4{0.f, 0.f, 0.f, 0.f};
   float dpc[KR];  // wave 0: dPhiC[c][gq + 4 k]
 #pragma unroll
   for (int k = 0; k < KR; ++k) dpc[k] = 0.f;
   double lsum = 0.0;
-  du_f32x4 TP[NT], VP[4];  // the previous sample's T and V (folded), for its epilogue
+  du_f32x4 TP[NT], VP[NVS];  // the previous sample's T and V (folded), for its epilogue
 #pragma unroll
   for (int q = 0; q < NT; ++q) TP[q] = du_f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int q = 0; q < 4; ++q) VP[q] = du_f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int q = 0; q < NVS; ++q) VP[q] = du_f32x4{0.f, 0.f, 0.f, 0.f};
   int64_t yP = 0;
   float cwP = 0.f;
 
@@ -862,7 +876,7 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
 #pragma unroll
       for (int q = 0; q < NT; ++q) gT[q] += E.e_wv * TP[q];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) gV[q] += E.e_wv * VP[q];
+      for (int q = 0; q < NVS; ++q) gV[q] += E.e_wv * VP[q];
       if constexpr (BLK) {
         if (lo8)
 #pragma unroll
@@ -893,7 +907,7 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
   auto src_of_group = [&](const float* p, int gi) { return GAFF ? p + 2048 * gi : p; };
   auto dma_sample = [&](const float* src, int slot) {
 #pragma unroll
-    for (int gi = 0; gi < 8; ++gi)
+    for (int gi = 0; gi < NG; ++gi)
       dma_piece(goff_of(gi), src_of_group(src, gi), lbase + (uint32_t)(slot * 4 * SPF) + (uint32_t)(wv + NW * gi) * 1024u);
   };
   // the kernel is bound by the bytes in flight per CU, not by its issue stream (no-LDS-DMA
@@ -928,8 +942,10 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
       const bool more = k + 1 < nr;
       if (!(TR_DUO_SKIP & 16)) yN = lab[sample_of(more ? k + 1 : k)];
     }
-    if (NS == 3)
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // own pieces of k (those of k + 1 may be in flight)
+    if (NS == 3 && J32)
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // own pieces of k (those of k + 1 may be in flight)
+    else if (NS == 3)
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     TR_DUO_MARK(0);
@@ -959,13 +975,13 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
     EpiSt E;
     if constexpr (bfirst) epi(E, 0, zsP, yP, cwP);
     const float* sb = lds + SL * SPF;
-    du_f32x4 aT[NT], aV[4];
+    du_f32x4 aT[NT], aV[NVS];
 #pragma unroll
     for (int q = 0; q < NT; ++q) aT[q] = du_f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int q = 0; q < 4; ++q) aV[q] = du_f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int q = 0; q < NVS; ++q) aV[q] = du_f32x4{0.f, 0.f, 0.f, 0.f};
     // every operand of sample k into registers
-    constexpr int NU = NT * NKT;  // T steps (4); then 4 V steps (one j-tile each)
+    constexpr int NU = NT * NKT;  // T steps (4; J = 32: 2); then NVS V steps (one j-tile each)
     du_f32x4 xv[8], xt[NU][2];
 #pragma unroll
     for (int e = 0; e < 8; ++e) xv[e] = *reinterpret_cast<const du_f32x4*>(sb + vro[e]);
@@ -977,7 +993,7 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
       xt[u][1] = *reinterpret_cast<const du_f32x4*>(sb + tro[tt] + 4 * ((q0 + 1) ^ tsw));
     }
 #pragma unroll
-    for (int st = 0; st < NU + 4; ++st) {
+    for (int st = 0; st < NU + NVS; ++st) {
       if (!(TR_DUO_SKIP & 8)) dma_piece(goff_of(st), src_of_group(psrc, st), pm0 + (uint32_t)st * (uint32_t)(NW * 1024));
       sl_u4 x1, x2, x3;  // the k step's X pieces (pairs per VGPR)
       auto split = [&](float e0, float e1, int v) {
@@ -1031,12 +1047,28 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
       } else {
         const int tv = st - NU;  // j-tile: element tv of each row's chunk
 #pragma unroll
-        for (int v = 0; v < 4; ++v) split(xv[2 * v][tv], xv[2 * v + 1][tv], v);
+        for (int v = 0; v < 4; ++v) {
+          if constexpr (J32) {  // element tv (lanes n < 8) or tv + 2 (n >= 8) of each row's chunk
+            const bool hi = n >= 8;
+            split(hi ? xv[2 * v][tv + 2] : xv[2 * v][tv], hi ? xv[2 * v + 1][tv + 2] : xv[2 * v + 1][tv], v);
+          } else {
+            split(xv[2 * v][tv], xv[2 * v + 1][tv], v);
+          }
+        }
         gemm(aV[tv], bV12, bV2, bV3, hV);
       }
-      if (bfirst && st >= 1 && st <= 7) epi(E, st, zsP, yP, cwP);  // (bfirst, st: compile-time)
+      if constexpr (J32) {  // four steps: stages 1..6 two per step, 7 after them
+        if (bfirst && st >= 1) {
+          epi(E, 2 * st - 1, zsP, yP, cwP);
+          epi(E, 2 * st, zsP, yP, cwP);
+        }
+      } else {
+        if (bfirst && st >= 1 && st <= 7) epi(E, st, zsP, yP, cwP);  // (bfirst, st: compile-time)
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
+    if constexpr (J32)
+      if (bfirst) epi(E, 7, zsP, yP, cwP);
     TR_DUO_MARK(2);
     // fold the piece columns (rank r = column r + column r + 8), U partial of this wave -> LDS
     float u = BLK ? uacc : 0.f;
@@ -1061,14 +1093,14 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
     }
     if constexpr (BLK) {  // V over the blocks (folded at the last)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) aV[q] = bfirst ? aV[q] : VP[q] + aV[q];
+      for (int q = 0; q < NVS; ++q) aV[q] = bfirst ? aV[q] : VP[q] + aV[q];
       if (!blast)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) VP[q] = aV[q];
+        for (int q = 0; q < NVS; ++q) VP[q] = aV[q];
     }
     if (blast) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < NVS; ++q) {
 #pragma unroll
         for (int v = 0; v < 4; ++v)
           if constexpr (!R16) aV[q][v] += du_dpp<0x128>(aV[q][v]);
@@ -1136,10 +1168,12 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
             for (int v = 0; v < 4; ++v) sG[(bb * I + it0 + 16 * tt + 4 * gq + v) * R + r8] += gt[v];
           }
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
+      for (int q = 0; q < NVS; ++q)
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
-          const int j = 4 * (cv - n + 4 * gq + v) + q;  // chunk (row 4 gq + v of the tile) -> j = 4 chunk + tile
+          // chunk (row 4 gq + v of the tile) -> j = 4 chunk + tile (J = 32: tile row m -> j = 4 (m & 7) + q + 2 (m >> 3))
+          const int m = 4 * gq + v;
+          const int j = J32 ? 4 * (m & 7) + q + 2 * (m >> 3) : 4 * (cv - n + m) + q;
           if (!PAD || j < Jr) sG[g.offP1 + j * R + r8] += gV[q][v];
         }
     }
@@ -1162,9 +1196,10 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
 }
 
 // NW waves per workgroup, 8 / NW workgroups per CU (the second bound is waves per SIMD: two,
-// 256 VGPRs each), a ring of NS samples
+// 256 VGPRs each), a ring of NS samples; J = 32 at NW <= 6: 12 / NW workgroups, three waves per SIMD
+// of 168 VGPRs (its per-sample epilogue is twice the VALU work per byte of the 64-wide form's)
 template <int JT, int NW, int NS, bool PAD, bool EXACT, int NB, int RK>
-__global__ __launch_bounds__(NW * TR_WAVE, 2) void k_mnl_bsp(MnlGeom g, DuArgs a, const int64_t* __restrict__ lab,
+__global__ __launch_bounds__(NW * TR_WAVE, JT == 32 && NW <= 6 ? 3 : 2) void k_mnl_bsp(MnlGeom g, DuArgs a, const int64_t* __restrict__ lab,
                                                                const float* __restrict__ class_w,
                                                                const int32_t* __restrict__ stop) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -1188,10 +1223,12 @@ __global__ __launch_bounds__(DU_T, 2) void k_mnl_duo(MnlGeom g, DuArgs a, const 
 // host side
 // ------------------------------------------------------------------------------------------
 // the split body's instantiations (J, NW, ring slots): (32 NW, 64) samples with NW = 2..8, (16 NW,
-// 128) with NW = 4, 6, 8; a ring of three at NW = 5, 6
+// 128) with NW = 4, 6, 8; a ring of three at NW = 5, 6; (32 NW, 32) with NW = 2..8, rings of two and three
 #define TR_BSP_LIST(X) \
   X(64, 2, 2) X(64, 3, 2) X(64, 4, 2) X(64, 5, 2) X(64, 5, 3) X(64, 6, 2) X(64, 6, 3) X(64, 7, 2) \
-  X(64, 8, 2) X(128, 4, 2) X(128, 6, 2) X(128, 6, 3) X(128, 8, 2)
+  X(64, 8, 2) X(128, 4, 2) X(128, 6, 2) X(128, 6, 3) X(128, 8, 2)                                 \
+  X(32, 2, 2) X(32, 2, 3) X(32, 3, 2) X(32, 3, 3) X(32, 4, 2) X(32, 4, 3) X(32, 5, 2) X(32, 5, 3) \
+  X(32, 6, 2) X(32, 6, 3) X(32, 7, 2) X(32, 7, 3) X(32, 8, 2) X(32, 8, 3)
 // ... and its row-block instantiations (J, NW, ring slots, blocks): samples of NB blocks of 32 NW x
 // 64 or 16 NW x 128 rows.  (At (64, 8) only two blocks fit the LDS; (128, 8) with three and every
 // four-block form spill: such samples, e.g. (384, 128), (512, 128), (768, 64), run the two-pass kernels.)
@@ -1253,11 +1290,14 @@ static int64_t duo_carve(MnlGeom* g, int nw, int64_t spf, int ns) {
   g->bs_oU = (int)o;  // bsp: [ns][NW waves][bs_rk ranks] U partials
   o += ns * nw * (g->bs_rk == 16 ? 16 : 8);
   g->bs_oTB = (int)o;  // bsp row blocks: [2][nb - 1][NW][NT][128] (T, dPhi0) of the earlier blocks
-  if (g->du_nb > 1) o += 2LL * (g->du_nb - 1) * nw * (g->du_jt == 64 ? 2 : 1) * 128;
+  if (g->du_nb > 1) o += 2LL * (g->du_nb - 1) * nw * (g->du_jt == 128 ? 1 : 2) * 128;
   g->du_oG = g->slab <= ns * spf ? 0 : (int)o;  // the arena image aliases the drained ring
   if (g->du_oG) o += g->slab;
   return (o + 3) & ~(int64_t)3;
 }
+
+// the narrowest sample the split body takes (the 32-wide form, padded up to J = 32)
+constexpr int kBspJ32Min = 24;
 
 void mnl_duo_geom(MnlGeom* g) {
   g->duo = 0;
@@ -1274,9 +1314,13 @@ void mnl_duo_geom(MnlGeom* g) {
   if (env != nullptr && env[0] == '0') return;
   // (J from 28 up: padded to 64, J = 32 runs at 46-48 % of HBM against 14-37 % on the fallbacks; at
   // J = 24 and 16 the two-pass kernels are faster, 34 vs 29 % and 34 vs 25 %, tools/mnl_shapes.py)
-  if (g->C > kMnlCMax || g->J % 4 != 0 || g->J < 28 || g->J > 128) return;
-  // the compiled row width: J itself (64, 128) or the next one up (a padded sample)
-  const int jt = g->J <= 64 ? 64 : 128;
+  if (g->C > kMnlCMax || g->J % 4 != 0 || g->J < kBspJ32Min || g->J > 128) return;
+  // the compiled row width: J itself (32, 64, 128) or the next one up (a padded sample).  32 for
+  // samples of up to 256 rows at rank <= 8 (the 32-wide body has no row-block or 16-rank forms);
+  // J = 28..32 beyond those padded to 64 as before
+  const bool j32 = g->J <= 32 && g->I <= 256 && g->R <= 8;
+  if (g->J < 28 && !j32) return;
+  const int jt = j32 ? 32 : g->J <= 64 ? 64 : 128;
   // compiled shapes: the rank-block body takes a 32 KiB sample as (128, 64) or (64, 128) (two
   // 64-row blocks, 8 LDS-DMA groups per wave, chunk swizzle q ^ (i & 15)); the split body takes
   // those, every (32 NW, 64) sample with NW = 2..8 (one wave per 32 rows) and every (16 NW, 128)
@@ -1286,7 +1330,7 @@ void mnl_duo_geom(MnlGeom* g) {
   // row of the sample and meet zero Phi0 rows)
   // (any I up to the wave-row ceiling: a sample of a few rows still runs 3.6-4x faster padded to
   // two wave rows than on the fused kernel, whose cost per sample does not fall with I)
-  const bool wide = (jt == 64 && g->I <= 256) || (jt == 128 && g->I <= 128);
+  const bool wide = (jt <= 64 && g->I <= 256) || (jt == 128 && g->I <= 128);
   // form: the f32 rank-block body where it fits (R in 5..8: two rank blocks), the bf16-split body
   // for R <= 4 and for the other (I, 64) shapes; TR_DUO_SPLIT=1 takes the split body for R <= 8,
   // =0 the rank-block body only.  (With the non-temporal sample DMA both run at the same rate at
@@ -1318,11 +1362,12 @@ void mnl_duo_geom(MnlGeom* g) {
     g->du_nb = 1;
     return;
   }
-  const int nw = !bsp ? 4 : blk_nw ? blk_nw : jt == 64 ? (g->I > 32 ? (g->I + 31) / 32 : 2) : (g->I > 64 ? 2 * ((g->I + 31) / 32) : 4);
+  const int nw = !bsp ? 4 : blk_nw ? blk_nw : jt <= 64 ? (g->I > 32 ? (g->I + 31) / 32 : 2) : (g->I > 64 ? 2 * ((g->I + 31) / 32) : 4);
   g->du_jt = bsp ? jt : g->J;
-  const int wpc = 8 / nw;
+  // workgroups per CU: eight waves (two per SIMD), twelve for the 32-wide form at NW <= 6
+  const int wpc = jt == 32 && nw <= 6 ? 12 / nw : 8 / nw;
   // LDS floats per (padded) sample, or per row block
-  const int64_t spf = (int64_t)(!bsp ? g->I : jt == 64 ? 32 * nw : 16 * nw) * g->du_jt;
+  const int64_t spf = (int64_t)(!bsp ? g->I : jt <= 64 ? 32 * nw : 16 * nw) * g->du_jt;
   // a padded sample fills at least a third of its padded shape (TR_DUO_ANYFILL=1: any fill, for the
   // tests): below that the two-pass kernels' ~2.6 TB/s on the real bytes beats the body's rate on
   // the padded ones ((16, 64): 25.8 vs 32.3 % of HBM, (24, 48) at 0.28 even, (24, 64) at 0.375 37.5 vs
@@ -1334,7 +1379,9 @@ void mnl_duo_geom(MnlGeom* g) {
   // a ring of three samples: (160, 64) 58.9 -> 61.4 %, (192, 64) 65.4 -> 68.5 %, (96, 128) 65.8 ->
   // 69.7 % of HBM (tools/mnl_shapes.py, two runs each); at NW = 3 (two workgroups per CU) three
   // slots measured the same as two.
-  const bool ring3_ok = bsp && g->du_nb == 1 && (nw == 5 || nw == 6) && (jt == 64 || (nw == 6 && g->bs_rk == 8));
+  // The 32-wide body (half the bytes per slot) takes a ring of three at every NW.
+  const bool ring3_ok =
+      bsp && g->du_nb == 1 && (jt == 32 || ((nw == 5 || nw == 6) && (jt == 64 || (nw == 6 && g->bs_rk == 8))));
   int ns = 2;
   if (ring3_ok && wpc * carve(3) * 4 <= 160 * 1024) ns = 3;
   const int64_t o = carve(ns);
@@ -1379,7 +1426,7 @@ hipError_t mnl_duo_prepare(MnlGeom* g) {
   if (e != hipSuccess) return e;
   if (ok) return hipSuccess;
   if (g->bsp && g->du_ns == 3) {  // a ring of two instead (the three-slot instantiation spills)
-    const int64_t spf = (int64_t)(g->du_jt == 64 ? 32 : 16) * g->du_nw * g->du_jt;
+    const int64_t spf = (int64_t)(g->du_jt <= 64 ? 32 : 16) * g->du_nw * g->du_jt;
     g->du_ns = 2;
     g->du_lds_floats = (int)duo_carve(g, g->du_nw, spf, 2);
     e = duo_kernel_ok(*g, &ok);

@@ -273,8 +273,15 @@ MNL_GEOMETRY = [
     ((384, 64, 5), (1, 1, 6, 1, 2, 0, 64, 2, 8)),
     ((288, 128, 8), (1, 1, 6, 1, 2, 0, 128, 3, 8)),
     ((512, 48, 8), (1, 1, 8, 1, 2, 1, 64, 2, 8)),
+    ((64, 32, 4), (1, 1, 2, 6, 3, 0, 32, 1, 8)),       # the 32-wide form: ring of three, 12 waves per CU
+    ((256, 32, 8), (1, 1, 8, 1, 3, 0, 32, 1, 8)),
+    ((192, 32, 8), (1, 1, 6, 2, 3, 0, 32, 1, 8)),
+    ((100, 24, 4), (1, 1, 4, 3, 3, 1, 32, 1, 8)),      # padded rows and width
+    ((64, 24, 8), (1, 1, 2, 6, 3, 1, 32, 1, 8)),
+    ((128, 32, 12), (1, 1, 4, 2, 2, 1, 64, 1, 16)),    # rank > 8: the 64-wide 16-rank form
+    ((512, 32, 4), (1, 1, 8, 1, 2, 1, 64, 2, 8)),      # > 256 rows: 64-wide row blocks
 ]
-MNL_GEOMETRY_OUTSIDE = [(768, 64, 8), (300, 128, 8), (512, 128, 8), (256, 128, 12), (16, 64, 8), (64, 24, 8),
+MNL_GEOMETRY_OUTSIDE = [(768, 64, 8), (300, 128, 8), (512, 128, 8), (256, 128, 12), (16, 64, 8), (64, 12, 8), (32, 20, 8), (64, 20, 8),
                         (128, 64, 17)]
 
 
@@ -293,7 +300,7 @@ def test_mnl_geometry_envelope(shape, want, monkeypatch):
 @pytest.mark.parametrize("shape", MNL_GEOMETRY_OUTSIDE)
 def test_mnl_geometry_outside(shape, monkeypatch):
     """Outside the family: rows not whole blocks or four blocks (768, 64), (512, 128); rank > 8 with
-    row blocks; a sample filling less than a third of its padded shape; J < 28; rank > 16."""
+    row blocks; a sample filling less than a third of its padded shape; J < 16; rank > 16."""
     for k in ("TR_MNL_DUO", "TR_DUO_SPLIT", "TR_DUO_ANYFILL"):
         monkeypatch.delenv(k, raising=False)
     rc, g = _mnl_geometry(*shape)

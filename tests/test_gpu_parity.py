@@ -501,12 +501,24 @@ R16_OUTSIDE = [((40, 120, 128), 4, 12)]
 ROWBLOCK_OUTSIDE = [((40, 300, 128), 4, 8), ((30, 512, 128), 3, 5), ((30, 768, 64), 5, 4)]
 
 
-def _split_jt(J):
-    return 64 if J <= 64 else 128
+def _split_jt(I, J, rank=8):
+    """The split body's compiled row width: 32 (J <= 32, I <= 256, rank <= 8; round 6), 64, 128."""
+    return 32 if J <= 32 and I <= 256 and rank <= 8 else 64 if J <= 64 else 128
 
 
-def _split_waves(I, J):
-    return max(2, (I + 31) // 32) if _split_jt(J) == 64 else max(4, 2 * ((I + 31) // 32))
+def _split_waves(I, J, rank=8):
+    return max(2, (I + 31) // 32) if _split_jt(I, J, rank) <= 64 else max(4, 2 * ((I + 31) // 32))
+
+
+# (shape, C, rank, waves) on the split body's 32-wide form (J = 24..32, round 6; before it J = 28..32
+# ran padded to 64 and J < 28 on the two-pass kernels): every wave count, padded widths and rows, one
+# class, fewer samples than workgroups; a ring of three throughout
+J32_SHAPES = [((300, 64, 32), 10, 8, 2), ((200, 128, 24), 5, 4, 4), ((150, 256, 24), 7, 6, 8),
+              ((120, 96, 28), 3, 3, 3), ((90, 160, 32), 16, 5, 5), ((80, 224, 28), 4, 7, 7),
+              ((100, 192, 32), 1, 2, 6), ((7, 64, 32), 3, 8, 2), ((256, 256, 32), 10, 8, 8),
+              ((130, 100, 32), 6, 1, 4), ((60, 48, 24), 2, 3, 2)]
+# ... and narrow samples outside it: J < 24, rank > 8 (the 64-wide 16-rank form), more than 256 rows
+J32_OUTSIDE = [((100, 64, 12), 4, 3, "2pass"), ((100, 64, 20), 4, 3, "2pass"), ((80, 128, 32), 5, 12, "rk16"), ((40, 512, 32), 3, 4, "rowblocks")]
 MNL_SHAPES = [((50, 8, 4), 2, 2), ((200, 16, 8), 10, 4), ((97, 5, 7), 16, 3), ((64, 33), 3, 1),
               ((128, 4, 4, 4), 5, 6), ((333, 32, 32), 10, 8), ((40, 64), 16, 2), ((3, 32), 3, 2),
               # factored single pass: ragged 64-blocks, R % 4 != 0, k ranges split over 2 blocks,
@@ -522,6 +534,8 @@ MNL_SHAPES = [((50, 8, 4), 2, 2), ((200, 16, 8), 10, 4), ((97, 5, 7), 16, 3), ((
               *[r[:3] for r in ROWBLOCK_SHAPES], *ROWBLOCK_OUTSIDE,
               # ... and at ranks 9..16 (the 16-rank form; k_mnl_fused or two-pass before round 6)
               *[r[:3] for r in R16_SHAPES], *R16_OUTSIDE,
+              # ... and 32 wide (J = 24..32)
+              *[r[:3] for r in J32_SHAPES], *[r[:3] for r in J32_OUTSIDE],
               # wide classes (C > 16): logits by class tile (MFMA when P % 32 == 0, else VALU),
               # k_softmax_rows, tiled column reduction; rank beyond 64 (MTTKRP rank tiles)
               ((150, 8, 4), 17, 3), ((230, 16, 8), 40, 5), ((99, 5, 7), 33, 2), ((200, 12), 100, 4),
@@ -543,9 +557,9 @@ def test_multinomial_wide_split_body_selected(shape, C, rank, monkeypatch):
     of its padded shape runs the two-pass kernels by default and the split body with
     TR_DUO_ANYFILL=1."""
     monkeypatch.delenv("TR_DUO_ANYFILL", raising=False)
-    nw = _split_waves(shape[1], shape[2])
-    jt = _split_jt(shape[2])
-    if 3 * shape[1] * shape[2] < (32 if jt == 64 else 16) * nw * jt:
+    nw = _split_waves(shape[1], shape[2], rank)
+    jt = _split_jt(shape[1], shape[2], rank)
+    if 3 * shape[1] * shape[2] < (16 if jt == 128 else 32) * nw * jt:
         with path("auto"):
             desc = _multinomial_sweep(shape, C, rank)
         assert " duo " not in desc and "path=2pass" in desc, desc
@@ -554,8 +568,31 @@ def test_multinomial_wide_split_body_selected(shape, C, rank, monkeypatch):
         desc = _multinomial_sweep(shape, C, rank)
     # (round 5's padded (16 NW, 128) body with a ring of three spilled at NW = 6 and the plan took two
     # slots; round 6's epilogue fetches Wv and U by ds_bpermute instead of 12 select registers)
-    nbuf = 3 if nw in (5, 6) else 2
-    assert "form=bf16split" in desc and f"waves={nw} wg/cu={8 // nw} nbuf={nbuf} " in desc, desc
+    nbuf = 3 if nw in (5, 6) or jt == 32 else 2
+    wpc = 12 // nw if jt == 32 and nw <= 6 else 8 // nw
+    assert "form=bf16split" in desc and f"waves={nw} wg/cu={wpc} nbuf={nbuf} " in desc, desc
+
+
+@pytest.mark.parametrize("shape,C,rank,nw", J32_SHAPES)
+def test_multinomial_j32_form_selected(shape, C, rank, nw):
+    """Samples of J = 24..32 columns and up to 256 rows at rank <= 8 take the split body's 32-wide form
+    (describe 'jt=32') with a ring of three; the results are the sweep's (every kind runs on these
+    shapes in test_multinomial_sweep_vs_oracle)."""
+    with path("auto"):
+        desc = _multinomial_sweep(shape, C, rank)
+    wpc = 12 // nw if nw <= 6 else 1
+    assert "form=bf16split" in desc and f"waves={nw} wg/cu={wpc} nbuf=3 " in desc and " jt=32" in desc, desc
+
+
+@pytest.mark.parametrize("shape,C,rank,where", J32_OUTSIDE)
+def test_multinomial_j32_outside(shape, C, rank, where):
+    with path("auto"):
+        desc = _multinomial_sweep(shape, C, rank)
+    assert " jt=32" not in desc, desc
+    if where == "2pass":
+        assert " duo " not in desc and "path=2pass" in desc, desc
+    else:
+        assert " rk=16" in desc if where == "rk16" else "rowblocks=2" in desc, desc
 
 
 @pytest.mark.parametrize("shape,C,rank,nw,nb", ROWBLOCK_SHAPES)
