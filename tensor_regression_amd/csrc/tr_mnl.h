@@ -58,6 +58,7 @@ struct MnlGeom {
   // split body's row blocks per sample (1; a sample of du_nb * 32 NW (J <= 64) or du_nb * 16 NW rows
   // streams through the ring one row block per slot) and the LDS offset of the earlier blocks' T / dPhi0
   int du_nb, bs_oTB;
+  int bs_oW;  // bsp: [ns][8] published Wv of the one-wave epilogue (J = 32), then [8] per-wave loss partials (double)
   // split body's rank columns: 8 (R <= 8: two pieces of 8 ranks per 16-column tile, folded) or 16
   // (R 9..16: 16 ranks of one piece per tile)
   int bs_rk;

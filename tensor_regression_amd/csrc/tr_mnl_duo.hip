@@ -591,6 +591,14 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
   static_assert(NG == NT * NKT + NVS, "one LDS-DMA piece per GEMM step");
   static_assert(!J32 || (NB == 1 && RK == 8), "J = 32: one block, 8 rank columns");
   auto swz = [](int i) { return J32 ? ((i >> 1) + 2) & 7 : i & 15; };
+  // DIST (J = 32): the epilogue of sample s runs on wave s % NW alone (every wave ran every sample's:
+  // at 4 KiB of sample per wave its VALU work was a quarter of the kernel, profiles/r06_mnl_j32), which
+  // publishes Wv(s) in LDS; every wave applies it to its T(s), V(s) after the next barrier, one
+  // iteration later than the owner's stages (T, V of two samples live across the loop's back edge)
+  constexpr bool DIST = J32;
+  static_assert(!DIST || NB == 1, "one-wave epilogue: one block");
+  float* sWv = lds + g.bs_oW;  // [NS][8] Wv, then [NW] double loss partials
+  double* sLs = reinterpret_cast<double*>(sWv + NS * 8);
   const int R = g.R, C = g.C;
   // PAD: the sample's g.I x g.J (g.J % 4 == 0) fills only part of the compiled I x J; the padding
   // rows and column chunks read the sample's first chunk (valid memory) and meet zero Phi0 / Phi1 rows
@@ -717,7 +725,7 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
   // epilogue weights: pc[r] = w_r PhiC[c][r]; row gq's ranks gq + 4 k.  BLK, RK = 16 and J = 32 read them
   // from an LDS table in the rank-block body's Phi1 slots (unused here) in the epilogue: those forms
   // need the registers
-  constexpr bool PCL = BLK || R16 || J32;  // pc[] from the LDS table (J = 32: three waves per SIMD)
+  constexpr bool PCL = BLK || R16 || J32;  // pc[] from the LDS table
   float pc[8];
 #pragma unroll
   for (int r = 0; r < 8; ++r) pc[r] = (!PCL && cok && r < R) ? a.w[r] * PC[c * R + r] : 0.f;
@@ -737,6 +745,8 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
   auto pcg_of = [&](int k) { return PCL ? sPC[RK * c + gq + 4 * k] : pcg[k]; };
   auto wg_of = [&](int k) { return PCL ? sPC[16 * RK + gq + 4 * k] : wg[k]; };
   for (int e = t; e < NS * NW * RK; e += NT_) sU[e] = 0.f;
+  if constexpr (DIST)
+    for (int e = t; e < NS * 8; e += NT_) sWv[e] = 0.f;
   // BLK: the folded T of blocks 0 .. nb - 2 of the previous sample and this wave's dPhi0 rows of
   // those blocks, [2][nb - 1][NW][NT][gq][rank 8][v 4] (lanes n < 8 only; the last block's in registers)
   float* sTB = lds + g.bs_oTB;
@@ -791,10 +801,24 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
   for (int k = 0; k < KR; ++k) dpc[k] = 0.f;
   double lsum = 0.0;
   du_f32x4 TP[NT], VP[NVS];  // the previous sample's T and V (folded), for its epilogue
+  du_f32x4 TN[NT], VN[NVS];  // DIST: this sample's, from the fold to the next iteration's top
 #pragma unroll
-  for (int q = 0; q < NT; ++q) TP[q] = du_f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int q = 0; q < NT; ++q) TP[q] = TN[q] = du_f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int q = 0; q < NVS; ++q) VP[q] = du_f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int q = 0; q < NVS; ++q) VP[q] = VN[q] = du_f32x4{0.f, 0.f, 0.f, 0.f};
+  // DIST: Wv of the sample in ring slot zs (published by its owner) onto the held T, V; then the
+  // newest sample's T, V are the held ones
+  auto dist_apply = [&](int zs) {
+    const float wa = sWv[zs * 8 + r8];
+#pragma unroll
+    for (int q = 0; q < NT; ++q) gT[q] += wa * TP[q];
+#pragma unroll
+    for (int q = 0; q < NVS; ++q) gV[q] += wa * VP[q];
+#pragma unroll
+    for (int q = 0; q < NT; ++q) TP[q] = TN[q];
+#pragma unroll
+    for (int q = 0; q < NVS; ++q) VP[q] = VN[q];
+  };
   int64_t yP = 0;
   float cwP = 0.f;
 
@@ -857,7 +881,7 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
       const float is2 = __builtin_amdgcn_rcpf(E.e_s2);
       const float kk = cwE * a.scale;
       const float dot = kk * (E.e_d1 * is2 - E.e_e1);
-      lsum += (wv == 0 && lane == 0) ? (double)cwE * (double)(du_log(E.e_s2) - E.e_e1) : 0.0;
+      lsum += ((DIST || wv == 0) && lane == 0) ? (double)cwE * (double)(du_log(E.e_s2) - E.e_e1) : 0.0;
       const float dS = cok ? kk * (E.e_q * is2 - (E.e_isy ? 1.0f : 0.0f)) : 0.f;
       E.e_dz = cok ? E.e_S * (dS - dot) : 0.f;
 #pragma unroll
@@ -872,6 +896,8 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
         E.e_wv = r8 < 8 ? (r8 < 4 ? wk[0] : wk[1]) : (r8 < 12 ? wk[2] : wk[3]);
       else
         E.e_wv = r8 < 4 ? wk[0] : wk[1];
+    } else if (DIST) {  // publish Wv (lanes r < 8); every wave applies it after the next barrier
+      if (lane < 8) sWv[zs * 8 + lane] = E.e_wv;
     } else {
 #pragma unroll
       for (int q = 0; q < NT; ++q) gT[q] += E.e_wv * TP[q];
@@ -888,7 +914,9 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
               *gp += E.e_wv * tp;
             }
       }
-      if (wv == 0) {  // dPhiC[c][r] += dZ[c] w_r U[r], r = gq + 4 k
+    }
+    if (st == 7) {
+      if (DIST || wv == 0) {  // dPhiC[c][r] += dZ[c] w_r U[r], r = gq + 4 k (DIST: the owner's partial)
 #pragma unroll
         for (int k = 0; k < KR; ++k) {
           const float uk = __int_as_float(__builtin_amdgcn_ds_bpermute(4 * gq + 16 * k, __float_as_int(E.uS)));  // U[gq + 4 k]
@@ -959,6 +987,7 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
     } else {
       cwC = du_rdl(cwl, (int)yC);
     }
+    if constexpr (DIST) dist_apply((SL + 2 * NS - 2) % NS);  // Wv(k - 2), published at the end of k - 1
     // sample k + 2 into this slot once it is read (past the end: a harmless refill of a valid sample)
     const int kd = k + NS - 1;  // the sample this iteration's DMA brings in
     constexpr int PS = (SL + NS - 1) % NS;     // slot of sample k - 1 (and of the DMA's target)
@@ -973,7 +1002,9 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
     // U partial slots: per ring slot (!BLK), per sample parity (BLK)
     const int zsP = BLK ? ((k - 1) & 1) : PS, zsC = BLK ? (k & 1) : SL;
     EpiSt E;
-    if constexpr (bfirst) epi(E, 0, zsP, yP, cwP);
+    // DIST: this wave runs the epilogue of k - 1 if it owns that sample
+    const bool own = !DIST || (k + NW - 1) % NW == wv;
+    if (bfirst && own) epi(E, 0, zsP, yP, cwP);
     const float* sb = lds + SL * SPF;
     du_f32x4 aT[NT], aV[NVS];
 #pragma unroll
@@ -1058,7 +1089,7 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
         gemm(aV[tv], bV12, bV2, bV3, hV);
       }
       if constexpr (J32) {  // four steps: stages 1..6 two per step, 7 after them
-        if (bfirst && st >= 1) {
+        if (bfirst && st >= 1 && own) {
           epi(E, 2 * st - 1, zsP, yP, cwP);
           epi(E, 2 * st, zsP, yP, cwP);
         }
@@ -1068,7 +1099,7 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
       __builtin_amdgcn_sched_barrier(0);
     }
     if constexpr (J32)
-      if (bfirst) epi(E, 7, zsP, yP, cwP);
+      if (bfirst && own) epi(E, 7, zsP, yP, cwP);
     TR_DUO_MARK(2);
     // fold the piece columns (rank r = column r + column r + 8), U partial of this wave -> LDS
     float u = BLK ? uacc : 0.f;
@@ -1079,7 +1110,9 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
         if constexpr (!R16) aT[tt][v] += du_dpp<0x128>(aT[tt][v]);  // row_ror:8
         u = fmaf(phiU[tt][v], aT[tt][v], u);
       }
-      if (blast) {
+      if (blast && DIST) {
+        TN[tt] = aT[tt];
+      } else if (blast) {
         TP[tt] = aT[tt];
       } else if (lo8) {  // (BLK) block b's T until the sample's epilogue
         *reinterpret_cast<du_f32x4*>(sTB + tb_at(b, tt)) = aT[tt];
@@ -1104,7 +1137,10 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
 #pragma unroll
         for (int v = 0; v < 4; ++v)
           if constexpr (!R16) aV[q][v] += du_dpp<0x128>(aV[q][v]);
-        VP[q] = aV[q];
+        if constexpr (DIST)
+          VN[q] = aV[q];
+        else
+          VP[q] = aV[q];
       }
       u = du_xor32_sum(du_xor16_sum(u));  // lane (n < RK, any row): this wave's U partial of rank n
       if (lane < RK) sU[zsC * (RK * NW) + wv * RK + lane] = u;
@@ -1139,11 +1175,22 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
 #endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last (harmless) refill has landed
   du_barrier();  // U partials of the last sample
-  if (nr > 0) {
+  if (DIST && nr > 0) {  // Wv(nr - 2) onto its T, V; the last sample's epilogue on its owner; its Wv
+    dist_apply((nr + NS - 2) % NS);
+    if ((nr - 1) % NW == wv) {
+      EpiSt E;
+#pragma unroll
+      for (int st = 0; st < 8; ++st) epi(E, st, (nr - 1) % NS, yP, cwP);
+    }
+    du_barrier();
+    dist_apply((nr - 1) % NS);
+  } else if (nr > 0) {
     EpiSt E;
 #pragma unroll
     for (int st = 0; st < 8; ++st) epi(E, st, BLK ? (nr - 1) & 1 : (nr - 1) % NS, yP, cwP);
   }
+  if constexpr (DIST)
+    if (lane == 0) sLs[wv] = lsum;  // (read after the reduction's barriers)
 
   // ---- fixed-order reduction into an LDS image of the arena (wave order), slab ----
   float* sG = lds + g.du_oG;
@@ -1177,7 +1224,7 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
           if (!PAD || j < Jr) sG[g.offP1 + j * R + r8] += gV[q][v];
         }
     }
-    if (ws == wv && wv == 0 && cok) {
+    if (ws == wv && (DIST || wv == 0) && cok) {
 #pragma unroll
       for (int k = 0; k < KR; ++k)
         if (gq + 4 * k < R) sG[g.offPC + c * R + gq + 4 * k] += dpc[k];
@@ -1185,7 +1232,13 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
     __syncthreads();
   }
   if (wv == 0) {
-    lsum = tr_wave_allreduce_d(lsum);
+    if constexpr (DIST) {  // the owners' partials in wave order
+      double s = 0.0;
+      for (int w = 0; w < NW; ++w) s += sLs[w];
+      lsum = s;
+    } else {
+      lsum = tr_wave_allreduce_d(lsum);
+    }
     if (lane == 0) {
       a.dpart[2 * blockIdx.x] = lsum;
       a.dpart[2 * blockIdx.x + 1] = 0.0;
@@ -1196,10 +1249,11 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
 }
 
 // NW waves per workgroup, 8 / NW workgroups per CU (the second bound is waves per SIMD: two,
-// 256 VGPRs each), a ring of NS samples; J = 32 at NW <= 6: 12 / NW workgroups, three waves per SIMD
-// of 168 VGPRs (its per-sample epilogue is twice the VALU work per byte of the 64-wide form's)
+// 256 VGPRs each), a ring of NS samples.  (J = 32 at three waves per SIMD, 168 VGPRs with every
+// wave running every epilogue: 43-64 % of HBM; the one-wave epilogue at two: 53-68 %, and it does not
+// fit 168; profiles/r06_mnl_j32)
 template <int JT, int NW, int NS, bool PAD, bool EXACT, int NB, int RK>
-__global__ __launch_bounds__(NW * TR_WAVE, JT == 32 && NW <= 6 ? 3 : 2) void k_mnl_bsp(MnlGeom g, DuArgs a, const int64_t* __restrict__ lab,
+__global__ __launch_bounds__(NW * TR_WAVE, 2) void k_mnl_bsp(MnlGeom g, DuArgs a, const int64_t* __restrict__ lab,
                                                                const float* __restrict__ class_w,
                                                                const int32_t* __restrict__ stop) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -1289,6 +1343,8 @@ static int64_t duo_carve(MnlGeom* g, int nw, int64_t spf, int ns) {
   o = (o + 3) & ~(int64_t)3;
   g->bs_oU = (int)o;  // bsp: [ns][NW waves][bs_rk ranks] U partials
   o += ns * nw * (g->bs_rk == 16 ? 16 : 8);
+  g->bs_oW = (int)o;  // bsp one-wave epilogue (J = 32): [ns][8] Wv, [8] double loss partials
+  o += ns * 8 + 16;
   g->bs_oTB = (int)o;  // bsp row blocks: [2][nb - 1][NW][NT][128] (T, dPhi0) of the earlier blocks
   if (g->du_nb > 1) o += 2LL * (g->du_nb - 1) * nw * (g->du_jt == 128 ? 1 : 2) * 128;
   g->du_oG = g->slab <= ns * spf ? 0 : (int)o;  // the arena image aliases the drained ring
@@ -1364,8 +1420,7 @@ void mnl_duo_geom(MnlGeom* g) {
   }
   const int nw = !bsp ? 4 : blk_nw ? blk_nw : jt <= 64 ? (g->I > 32 ? (g->I + 31) / 32 : 2) : (g->I > 64 ? 2 * ((g->I + 31) / 32) : 4);
   g->du_jt = bsp ? jt : g->J;
-  // workgroups per CU: eight waves (two per SIMD), twelve for the 32-wide form at NW <= 6
-  const int wpc = jt == 32 && nw <= 6 ? 12 / nw : 8 / nw;
+  const int wpc = 8 / nw;  // workgroups per CU: eight waves, two per SIMD
   // LDS floats per (padded) sample, or per row block
   const int64_t spf = (int64_t)(!bsp ? g->I : jt <= 64 ? 32 * nw : 16 * nw) * g->du_jt;
   // a padded sample fills at least a third of its padded shape (TR_DUO_ANYFILL=1: any fill, for the

@@ -273,11 +273,11 @@ MNL_GEOMETRY = [
     ((384, 64, 5), (1, 1, 6, 1, 2, 0, 64, 2, 8)),
     ((288, 128, 8), (1, 1, 6, 1, 2, 0, 128, 3, 8)),
     ((512, 48, 8), (1, 1, 8, 1, 2, 1, 64, 2, 8)),
-    ((64, 32, 4), (1, 1, 2, 6, 3, 0, 32, 1, 8)),       # the 32-wide form: ring of three, 12 waves per CU
+    ((64, 32, 4), (1, 1, 2, 4, 3, 0, 32, 1, 8)),       # the 32-wide form, a ring of three
     ((256, 32, 8), (1, 1, 8, 1, 3, 0, 32, 1, 8)),
-    ((192, 32, 8), (1, 1, 6, 2, 3, 0, 32, 1, 8)),
-    ((100, 24, 4), (1, 1, 4, 3, 3, 1, 32, 1, 8)),      # padded rows and width
-    ((64, 24, 8), (1, 1, 2, 6, 3, 1, 32, 1, 8)),
+    ((192, 32, 8), (1, 1, 6, 1, 3, 0, 32, 1, 8)),
+    ((100, 24, 4), (1, 1, 4, 2, 3, 1, 32, 1, 8)),      # padded rows and width
+    ((64, 24, 8), (1, 1, 2, 4, 3, 1, 32, 1, 8)),
     ((128, 32, 12), (1, 1, 4, 2, 2, 1, 64, 1, 16)),    # rank > 8: the 64-wide 16-rank form
     ((512, 32, 4), (1, 1, 8, 1, 2, 1, 64, 2, 8)),      # > 256 rows: 64-wide row blocks
 ]

@@ -569,8 +569,7 @@ def test_multinomial_wide_split_body_selected(shape, C, rank, monkeypatch):
     # (round 5's padded (16 NW, 128) body with a ring of three spilled at NW = 6 and the plan took two
     # slots; round 6's epilogue fetches Wv and U by ds_bpermute instead of 12 select registers)
     nbuf = 3 if nw in (5, 6) or jt == 32 else 2
-    wpc = 12 // nw if jt == 32 and nw <= 6 else 8 // nw
-    assert "form=bf16split" in desc and f"waves={nw} wg/cu={wpc} nbuf={nbuf} " in desc, desc
+    assert "form=bf16split" in desc and f"waves={nw} wg/cu={8 // nw} nbuf={nbuf} " in desc, desc
 
 
 @pytest.mark.parametrize("shape,C,rank,nw", J32_SHAPES)
@@ -580,8 +579,7 @@ def test_multinomial_j32_form_selected(shape, C, rank, nw):
     shapes in test_multinomial_sweep_vs_oracle)."""
     with path("auto"):
         desc = _multinomial_sweep(shape, C, rank)
-    wpc = 12 // nw if nw <= 6 else 1
-    assert "form=bf16split" in desc and f"waves={nw} wg/cu={wpc} nbuf=3 " in desc and " jt=32" in desc, desc
+    assert "form=bf16split" in desc and f"waves={nw} wg/cu={8 // nw} nbuf=3 " in desc and " jt=32" in desc, desc
 
 
 @pytest.mark.parametrize("shape,C,rank,where", J32_OUTSIDE)
