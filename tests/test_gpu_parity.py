@@ -213,6 +213,8 @@ def _multinomial_golden(name, kind="auto"):
         want = "form=rankblock" if rb else "form=bf16split"
         assert want in plan.describe, plan.describe
         assert (" rk=16" in plan.describe) == (m["rank"] > 8), plan.describe
+        # (the 32-wide form, 'jt=32': J = 24..32, up to 256 rows, rank <= 8)
+        assert (" jt=32" in plan.describe) == (name.startswith("mnl_bsp_j32")), plan.describe
     cw, W = mm._class_weights(np.array(m["class_weights"]), dev, yd)
     arena = plan.pack(mm.Bcp)
     grad = torch.zeros(plan.num_grads, device=DEV)

@@ -507,6 +507,12 @@ def main():
              0.01, {'lr': 0.01}, 30)
     mnl_case("mnl_bsp_rowblk_256x128", 53, (8, 256, 128), 4, 8, [True, False, False], [1.0] * 4, 0.01,
              {'lr': 0.005}, 30, x_scale=2e-2)
+    # the split body's 32-wide form (round 6): (128, 32) rank 6 (four 32-row waves, a non-negative
+    # mode), and a padded (100, 24) sample (to (128, 32)) with full-mantissa X of small magnitude
+    mnl_case("mnl_bsp_j32_128x32", 54, (40, 128, 32), 5, 6, [False, True, False], [1.0, 2.0, 0.5, 1.0, 1.5],
+             0.01, {'lr': 0.01}, 30)
+    mnl_case("mnl_bsp_j32_pad_100x24", 55, (30, 100, 24), 4, 3, [False, False, False], [1.0, 0.5, 1.5, 1.0],
+             0.01, {'lr': 0.01, 'amsgrad': True}, 30, x_scale=2e-2)
     init_case("init_rng")
     spectral_case("spec_basic", 31, (64, 12, 9), 3, 2, 2, 1, False, 0.01, adam, 50)
     spectral_case("spec_nonneg_amsgrad_wd", 32, (80, 16, 17), 2, 3, 2, 2, [True, False, True], 0.02,
