@@ -118,7 +118,7 @@ def test_linear_full_size_vs_fp64(cfg):
 
 
 @pytest.mark.parametrize("form", ["bf16split", "rankblock", "fused", "wide64", "wide256", "wide128x128", "wide512",
-                                  "wide256x128", "rank16"])
+                                  "wide256x128", "rank16", "wide128x32", "wide256x32"])
 def test_multinomial_full_size_vs_fp64(form, monkeypatch):
     """Config 3: X (65536, 128, 64), 10 classes, rank 8 (the factored single pass: two 4-wave
     workgroups per CU in the f32 rank-block form (default) and the bf16-split form
@@ -127,7 +127,8 @@ def test_multinomial_full_size_vs_fp64(form, monkeypatch):
     samples (8 waves, one workgroup per CU, a shape k_mnl_fused does not fit) and on (128, 128)
     samples (8 waves of 16 rows) at the same sample bytes per GPU; wide512 / wide256x128: samples of
     128 KiB, (512, 64) and (256, 128), streamed through the split body in two row blocks of (256, 64) /
-    (128, 128) (round 6; the two-pass kernels before).  Bars: GRAD_TOL normwise, and no further from fp64 than the reference's own op sequence
+    (128, 128) (round 6; the two-pass kernels before); wide128x32 / wide256x32: the split body's 32-wide
+    form (4 and 8 waves, one-wave epilogue; round 6).  Bars: GRAD_TOL normwise, and no further from fp64 than the reference's own op sequence
     in fp32 on the host CPU (the oracle, same factors) is, x2 + 1e-7.  Measured (r05, worst
     gradient): rank-block 3.1e-7, split 7.2e-7, wide64 3.0e-7, wide256 1.47e-6, wide128x128
     1.53e-6; the reference in fp32 4.0e-6 (c3), 3.2e-6 (wide64), 9.8e-6 (wide256), 1.03e-5
@@ -162,10 +163,11 @@ def test_multinomial_full_size_vs_fp64(form, monkeypatch):
     assert "mnl-fused-1pass" in plan.describe
     assert (" duo " in plan.describe) == duo, plan.describe
     if form.startswith("wide"):
-        nw = min(8, I // 32 if J == 64 else I // 16)
-        nb = I // (32 * nw if J == 64 else 16 * nw)
+        nw = min(8, I // 16 if J == 128 else I // 32)
+        nb = I // (16 * nw if J == 128 else 32 * nw)
         assert "form=bf16split" in plan.describe and f"waves={nw} " in plan.describe, plan.describe
         assert (f"rowblocks={nb}" in plan.describe) == (nb > 1), plan.describe
+        assert (" jt=32" in plan.describe) == (J == 32), plan.describe
     elif form == "rank16":
         assert "form=bf16split" in plan.describe and " rk=16" in plan.describe, plan.describe
     elif duo:

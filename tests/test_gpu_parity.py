@@ -669,7 +669,8 @@ SPLIT_SCALE_SHAPES = [((300, 64, 64), 10, 8, "auto"), ((200, 96, 64), 7, 3, "aut
                       ((300, 100, 64), 10, 8, "auto"), ((200, 128, 48), 10, 8, "auto"), ((80, 70, 128), 4, 8, "auto"),
                       ((256, 128, 64), 10, 3, "auto"), ((256, 128, 64), 10, 8, "split"),
                       ((64, 256, 128), 10, 8, "auto"), ((40, 512, 64), 7, 5, "auto"),
-                      ((256, 128, 64), 10, 16, "auto"), ((150, 96, 128), 6, 12, "auto")]
+                      ((256, 128, 64), 10, 16, "auto"), ((150, 96, 128), 6, 12, "auto"),
+                      ((200, 128, 32), 10, 8, "auto"), ((150, 100, 24), 6, 5, "auto"), ((120, 256, 28), 4, 3, "auto")]
 
 
 @pytest.mark.parametrize("xscale", [1e-4, 1e-2, 1.0, 1e4, 3e7, "mixed"])
