@@ -722,10 +722,10 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
   };
   load_rows(0, phiU);
   if constexpr (!BLK) split_rows();
-  // epilogue weights: pc[r] = w_r PhiC[c][r]; row gq's ranks gq + 4 k.  BLK, RK = 16 and J = 32 read them
+  // epilogue weights: pc[r] = w_r PhiC[c][r]; row gq's ranks gq + 4 k.  BLK and RK = 16 read them
   // from an LDS table in the rank-block body's Phi1 slots (unused here) in the epilogue: those forms
   // need the registers
-  constexpr bool PCL = BLK || R16 || J32;  // pc[] from the LDS table
+  constexpr bool PCL = BLK || R16;  // pc[] from the LDS table
   float pc[8];
 #pragma unroll
   for (int r = 0; r < 8; ++r) pc[r] = (!PCL && cok && r < R) ? a.w[r] * PC[c * R + r] : 0.f;
@@ -886,6 +886,10 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
       E.e_dz = cok ? E.e_S * (dS - dot) : 0.f;
 #pragma unroll
       for (int k = 0; k < KR; ++k) E.e_w[k] = kk * (E.e_a[k] * is2 - E.e_y[k]) - dot * E.e_b[k];  // Wv[gq + 4 k]
+    } else if (st == 6 && DIST) {  // publish Wv: row gq's first lane holds Wv[gq + 4 k]
+      if (n == 0)
+#pragma unroll
+        for (int k = 0; k < KR; ++k) sWv[zs * 8 + gq + 4 * k] = E.e_w[k];
     } else if (st == 6) {
       // Wv[r] of this lane's accumulator rank r: row (r & 3)'s e_w[r >> 2], fetched from lane 16 (r & 3)
       const int src = 64 * (r8 & 3);
@@ -896,8 +900,7 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
         E.e_wv = r8 < 8 ? (r8 < 4 ? wk[0] : wk[1]) : (r8 < 12 ? wk[2] : wk[3]);
       else
         E.e_wv = r8 < 4 ? wk[0] : wk[1];
-    } else if (DIST) {  // publish Wv (lanes r < 8); every wave applies it after the next barrier
-      if (lane < 8) sWv[zs * 8 + lane] = E.e_wv;
+    } else if (DIST) {  // (Wv published at stage 6; every wave applies it after the next barrier)
     } else {
 #pragma unroll
       for (int q = 0; q < NT; ++q) gT[q] += E.e_wv * TP[q];
@@ -919,7 +922,16 @@ __device__ __forceinline__ void bsp_body(const MnlGeom& g, const DuArgs& a, cons
       if (DIST || wv == 0) {  // dPhiC[c][r] += dZ[c] w_r U[r], r = gq + 4 k (DIST: the owner's partial)
 #pragma unroll
         for (int k = 0; k < KR; ++k) {
-          const float uk = __int_as_float(__builtin_amdgcn_ds_bpermute(4 * gq + 16 * k, __float_as_int(E.uS)));  // U[gq + 4 k]
+          // U[gq + 4 k] (DIST: four uniform values by readlane and a select, no LDS round trip on the
+          // owner's chain; selecting among E.uR[] elements would put E in scratch)
+          float uk;
+          if constexpr (DIST) {
+            const float u0 = du_rdl(E.uS, 4 * k), u1 = du_rdl(E.uS, 4 * k + 1), u2 = du_rdl(E.uS, 4 * k + 2),
+                        u3 = du_rdl(E.uS, 4 * k + 3);
+            uk = gq < 2 ? (gq == 0 ? u0 : u1) : (gq == 2 ? u2 : u3);
+          } else {
+            uk = __int_as_float(__builtin_amdgcn_ds_bpermute(4 * gq + 16 * k, __float_as_int(E.uS)));
+          }
           dpc[k] = fmaf(E.e_dz, wg_of(k) * uk, dpc[k]);
         }
       }
