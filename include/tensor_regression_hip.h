@@ -149,9 +149,9 @@ int tr_plan_set_x_range(tr_plan* plan, double max_abs, double min_row_mean_sq, d
  * The multinomial factored pass's shape decision for two-mode samples (I, J), rank R, C classes,
  * without a device (ABI 8): out[0] = 1 if the two-workgroups-per-CU family (k_mnl_duo / k_mnl_bsp)
  * takes the shape, [1] = 1 for its bf16-split body (0: the rank-block body), [2] waves per
- * workgroup, [3] workgroups per CU, [4] ring slots, [5] 1 if padded, [6] compiled row width, [7]
- * row blocks per sample, [8] rank columns (8 or 16), [9] LDS bytes per workgroup, [10] 1 if
- * k_mnl_fused fits the shape.  A plan may still fall back (a spilling instantiation, found at plan
+ * workgroup, [3] workgroups per CU, [4] ring slots, [5] 1 if padded, [6] compiled row width (32,
+ * 64 or 128), [7] row blocks per sample, [8] rank columns (8 or 16), [9] LDS bytes per workgroup,
+ * [10] 1 if k_mnl_fused fits the shape.  A plan may still fall back (a spilling instantiation, found at plan
  * creation from the code object).  Reads the same environment switches as tr_plan_create.  n_out:
  * entries to write (at most 11).  Returns TR_E_UNSUPPORTED when no factored kernel fits at all.
  */
